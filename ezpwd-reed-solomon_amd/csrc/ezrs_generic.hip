@@ -1,0 +1,332 @@
+// ezrs_generic.hip -- per-codeword RS encode / decode kernels for every codec (GF(2^2)..GF(2^16)).
+//
+// One lane owns one codeword and runs the reference algorithm on it verbatim: the systematic LFSR
+// of encode_symbols (c++/ezpwd/rs_base:1296-1332) and the syndrome -> erasure locator ->
+// Berlekamp-Massey -> Chien -> Omega -> Forney chain of decode_symbols (rs_base:1335-1718), with the
+// data-type mapping of encode<INP>/decode<INP> (rs_base:868-904, 1170-1242).  These kernels define
+// the engine's semantics for all inputs (shortened codes, erasures, the overwhelmed regime) and are
+// the error-path back end of the fast GF(2^8) kernels; they are table-driven (log/antilog in LDS
+// for m <= 12, in L2-resident global memory above that).
+#include "ezrs_internal.hpp"
+
+namespace ezrs {
+namespace {
+
+constexpr int kBlock = 256;
+
+// x mod nn for x < 2^32 (Karn's fold, rs_base:648-657).
+__device__ __forceinline__ unsigned modnn(unsigned x, unsigned nn, unsigned mm) {
+    while (x >= nn) {
+        x -= nn;
+        x = (x >> mm) + (x & nn);
+    }
+    return x;
+}
+
+template <typename T> struct Tabs {
+    const uint16_t *A;   // alpha_to
+    const uint16_t *I;   // index_of
+    const uint8_t *ID;   // into_dual
+    const uint8_t *FD;   // from_dual
+};
+
+// Stage the field tables into LDS when they fit (m <= 12: 2 x 8 KiB), else read them from HBM/L2.
+template <bool LDS>
+__device__ __forceinline__ void stage_tables(const DevCodec &c, uint16_t *smem, const uint16_t *&A,
+                                             const uint16_t *&I, const uint8_t *&ID,
+                                             const uint8_t *&FD) {
+    if (LDS) {
+        uint16_t *sA = smem, *sI = smem + (c.nn + 1);
+        uint8_t *sD = reinterpret_cast<uint8_t *>(smem + 2 * (c.nn + 1));
+        for (unsigned i = threadIdx.x; i <= c.nn; i += blockDim.x) {
+            sA[i] = c.alpha_to[i];
+            sI[i] = c.index_of[i];
+        }
+        if (c.dual)
+            for (unsigned i = threadIdx.x; i < 256; i += blockDim.x) {
+                sD[i] = c.into_dual[i];
+                sD[256 + i] = c.from_dual[i];
+            }
+        __syncthreads();
+        A = sA; I = sI; ID = sD; FD = sD + 256;
+    } else {
+        A = c.alpha_to; I = c.index_of; ID = c.into_dual; FD = c.from_dual;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+template <typename T, int MAXR, bool LDS>
+__global__ void __launch_bounds__(kBlock) k_encode_generic(DevCodec c, EncodeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+    const uint16_t *A, *I;
+    const uint8_t *ID, *FD;
+    stage_tables<LDS>(c, smem, A, I, ID, FD);
+    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= a.ncw) return;
+    const T *data = static_cast<const T *>(a.data) + k * a.data_stride;
+    T *parity = static_cast<T *>(a.parity) + k * a.parity_stride;
+    const unsigned NR = c.nroots, nn = c.nn, mm = c.mm;
+
+    // Circular parity register: logical parity[j] lives at par[(head + j) % NR], so the
+    // reference's std::rotate (rs_base:1318) becomes a head increment.
+    uint16_t par[MAXR];
+    for (unsigned j = 0; j < NR; ++j) par[j] = 0;
+    unsigned head = 0;
+    for (unsigned i = 0; i < a.len; ++i) {
+        unsigned sym = static_cast<unsigned>(data[i]) & nn;        // masked copy (rs_base:893)
+        if (c.dual) sym = FD[sym];
+        const unsigned fb = I[sym ^ par[head]];
+        if (fb != nn) {
+            unsigned p = head + 1;
+            for (unsigned j = 1; j < NR; ++j, ++p) {
+                if (p >= NR) p -= NR;
+                par[p] ^= A[modnn(fb + c.genpoly[NR - j], nn, mm)];
+            }
+        }
+        par[head] = fb != nn ? A[modnn(fb + c.genpoly[0], nn, mm)] : 0;
+        if (++head == NR) head = 0;
+    }
+    for (unsigned j = 0, p = head; j < NR; ++j) {
+        unsigned v = par[p];
+        parity[j] = static_cast<T>(c.dual ? ID[v] : v);
+        if (++p == NR) p = 0;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// decode_symbols on one codeword.  Corrections are recorded and applied at the end: for the direct
+// path every recorded correction (the reference corrects in place, so partial corrections before a
+// failure persist, rs_base:1238-1241), for the masked path only when count > 0 (rs_base:1223-1234).
+template <typename T, int MAXR>
+__device__ int decode_one(const DevCodec &c, const uint16_t *__restrict__ A,
+                          const uint16_t *__restrict__ I, const uint8_t *ID, const uint8_t *FD,
+                          T *data, unsigned len, T *parity, const uint32_t *eras,
+                          unsigned no_eras, uint32_t *pos_out, T *corr_out) {
+    const unsigned NR = c.nroots, NN = c.nn, A0 = c.nn, mm = c.mm, LOAD = c.load;
+    const unsigned FCR = c.fcr, PRM = c.prim;
+    if (len == 0 || len > LOAD) return -1;                                    // 1375-1377
+    if (no_eras > NR) return -1;                                              // 1380-1382
+    for (unsigned i = 0; i < no_eras; ++i)
+        if (eras[i] >= len + NR) return -1;                                   // 1383-1387
+    if (c.masked)
+        for (unsigned i = 0; i < NR; ++i)
+            if (static_cast<unsigned>(parity[i]) & ~NN) return -1;            // 1215-1218
+    const unsigned pad = LOAD - len;
+
+    uint16_t syn[MAXR], lambda[MAXR + 1], b[MAXR + 1], t[MAXR + 1], omega[MAXR + 1];
+    uint16_t root[MAXR], loc[MAXR], fixv[MAXR], corrv[MAXR];
+    uint16_t fixp[MAXR];
+    uint8_t wrote[MAXR];              // corr[j] written by the reference's Forney loop
+    unsigned nfix = 0, nroot = 0;
+    int count = 0;
+    unsigned deg_lambda = 0, deg_omega = 0, r = no_eras, el = no_eras;
+
+    auto cnv = [&](unsigned x) -> unsigned {
+        x &= NN;
+        return c.dual ? FD[x] : x;
+    };
+    // syndromes by Horner over data then parity (1390-1414)
+    {
+        const unsigned s0 = cnv(data[0]);
+        for (unsigned i = 0; i < NR; ++i) syn[i] = (uint16_t)s0;
+        for (unsigned j = 1; j < len + NR; ++j) {
+            const unsigned x = cnv(j < len ? static_cast<unsigned>(data[j])
+                                           : static_cast<unsigned>(parity[j - len]));
+            for (unsigned i = 0; i < NR; ++i)
+                syn[i] = syn[i] == 0 ? (uint16_t)x
+                                     : (uint16_t)(x ^ A[modnn(I[syn[i]] + (FCR + i) * PRM, NN, mm)]);
+        }
+    }
+    unsigned syn_error = 0;
+    for (unsigned i = 0; i < NR; ++i) {
+        syn_error |= syn[i];
+        syn[i] = I[syn[i]];
+    }
+    if (!syn_error) return 0;                                                 // 1427-1434
+
+    for (unsigned i = 0; i <= NR; ++i) lambda[i] = 0;                        // 1436-1450
+    lambda[0] = 1;
+    if (no_eras > 0) {
+        lambda[1] = A[modnn(PRM * (NN - 1 - (eras[0] + pad)), NN, mm)];
+        for (unsigned i = 1; i < no_eras; ++i) {
+            const unsigned u = modnn(PRM * (NN - 1 - (eras[i] + pad)), NN, mm);
+            for (unsigned j = i + 1; j > 0; --j) {
+                const unsigned tmp = I[lambda[j - 1]];
+                if (tmp != A0) lambda[j] ^= A[modnn(u + tmp, NN, mm)];
+            }
+        }
+    }
+    for (unsigned i = 0; i <= NR; ++i) b[i] = I[lambda[i]];
+
+    while (++r <= NR) {                                                       // BM 1507-1546
+        unsigned discr_r = 0;
+        for (unsigned i = 0; i < r; ++i)
+            if (lambda[i] != 0 && syn[r - i - 1] != A0)
+                discr_r ^= A[modnn(I[lambda[i]] + syn[r - i - 1], NN, mm)];
+        discr_r = I[discr_r];
+        if (discr_r == A0) {
+            for (unsigned i = NR; i > 0; --i) b[i] = b[i - 1];
+            b[0] = (uint16_t)A0;
+        } else {
+            t[0] = lambda[0];
+            for (unsigned i = 0; i < NR; ++i)
+                t[i + 1] = b[i] != A0 ? (uint16_t)(lambda[i + 1] ^ A[modnn(discr_r + b[i], NN, mm)])
+                                      : lambda[i + 1];
+            if (2 * el <= r + no_eras - 1) {
+                el = r + no_eras - el;
+                for (unsigned i = 0; i <= NR; ++i)
+                    b[i] = lambda[i] == 0 ? (uint16_t)A0
+                                          : (uint16_t)modnn(I[lambda[i]] - discr_r + NN, NN, mm);
+            } else {
+                for (unsigned i = NR; i > 0; --i) b[i] = b[i - 1];
+                b[0] = (uint16_t)A0;
+            }
+            for (unsigned i = 0; i <= NR; ++i) lambda[i] = t[i];
+        }
+    }
+
+    for (unsigned i = 0; i <= NR; ++i) {                                      // 1549-1553
+        lambda[i] = I[lambda[i]];
+        if (lambda[i] != NN) deg_lambda = i;
+    }
+    {                                                                         // Chien 1555-1584
+        uint16_t *reg = t;
+        for (unsigned i = 0; i <= NR; ++i) reg[i] = lambda[i];
+        count = 0;
+        for (unsigned i = 1, k = c.iprim - 1; i <= NN; ++i, k = modnn(k + c.iprim, NN, mm)) {
+            unsigned q = 1;
+            for (unsigned j = deg_lambda; j > 0; --j)
+                if (reg[j] != A0) {
+                    reg[j] = (uint16_t)modnn(reg[j] + j, NN, mm);
+                    q ^= A[reg[j]];
+                }
+            if (q != 0) continue;
+            root[count] = (uint16_t)i;
+            loc[count] = (uint16_t)k;
+            if (++count == (int)deg_lambda) break;
+        }
+    }
+    if ((int)deg_lambda != count || deg_lambda == 0) { count = -1; goto finish; }   // 1577-1595
+
+    nroot = (unsigned)count;
+    for (unsigned j = 0; j < nroot; ++j) wrote[j] = 0;
+    deg_omega = deg_lambda - 1;                                               // 1596-1604
+    for (unsigned i = 0; i <= deg_omega; ++i) {
+        unsigned tmp = 0;
+        for (unsigned j = i + 1; j-- > 0;)
+            if (syn[i - j] != A0 && lambda[j] != A0) tmp ^= A[modnn(syn[i - j] + lambda[j], NN, mm)];
+        omega[i] = I[tmp];
+    }
+
+    for (unsigned j = (unsigned)count; j-- > 0;) {                           // Forney 1610-1690
+        const unsigned rj = root[j];
+        unsigned num1 = 0;
+        for (unsigned i = deg_omega + 1; i-- > 0;)
+            if (omega[i] != A0) num1 ^= A[modnn(omega[i] + i * rj, NN, mm)];
+        const unsigned num2 = A[modnn(rj * (FCR - 1) + NN, NN, mm)];
+        unsigned den = 0;
+        const unsigned top = deg_lambda < NR - 1 ? deg_lambda : NR - 1;
+        for (int i = (int)(top & ~1u); i >= 0; i -= 2)
+            if (lambda[i + 1] != A0) den ^= A[modnn(lambda[i + 1] + (unsigned)i * rj, NN, mm)];
+        if (den == 0) { count = -1; goto finish; }
+        if (num1 != 0) {
+            if (loc[j] < pad) { count = -1; goto finish; }
+            const unsigned cor = A[modnn(I[num1] + I[num2] + NN - I[den], NN, mm)];
+            unsigned cv = cor;
+            unsigned at, delta = cor;
+            if (loc[j] < NN - NR) {
+                at = loc[j] - pad;
+                if (c.dual) {
+                    const unsigned err_dua = static_cast<unsigned>(data[at]) & NN;
+                    delta = ID[FD[err_dua] ^ cor] ^ err_dua;
+                    cv = delta;
+                }
+            } else {
+                const unsigned pi = loc[j] - (NN - NR);
+                at = len + pi;
+                if (c.dual) {
+                    const unsigned err_dua = static_cast<unsigned>(parity[pi]);
+                    const unsigned err_cnv = FD[err_dua];
+                    delta = ID[err_cnv ^ cor] ^ err_dua;
+                    cv = cor;                                 // fix_cnv ^ err_cnv (1684)
+                }
+            }
+            corrv[j] = (uint16_t)cv;
+            wrote[j] = 1;
+            fixp[nfix] = (uint16_t)at;
+            fixv[nfix] = (uint16_t)delta;
+            ++nfix;
+        }
+    }
+
+finish:
+    if (!c.masked || count > 0)
+        for (unsigned f = 0; f < nfix; ++f) {
+            const unsigned at = fixp[f];
+            if (at < len) data[at] = static_cast<T>(data[at] ^ fixv[f]);
+            else parity[at - len] = static_cast<T>(parity[at - len] ^ fixv[f]);
+        }
+    if (corr_out)  // corr is passed straight through by decode<INP> in both paths (1222, 1240)
+        for (unsigned j = 0; j < nroot; ++j)
+            if (wrote[j]) corr_out[j] = static_cast<T>(corrv[j]);
+    if (pos_out && count > 0)
+        for (int i = 0; i < count; ++i) pos_out[i] = loc[i] - pad;
+    return count;
+}
+
+template <typename T, int MAXR, bool LDS>
+__global__ void __launch_bounds__(kBlock) k_decode_generic(DevCodec c, DecodeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+    const uint16_t *A, *I;
+    const uint8_t *ID, *FD;
+    stage_tables<LDS>(c, smem, A, I, ID, FD);
+    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= a.ncw) return;
+    T *data = static_cast<T *>(a.data) + k * a.data_stride;
+    T *parity = static_cast<T *>(a.parity) + k * a.parity_stride;
+    const uint32_t *eras = a.eras ? a.eras + k * a.eras_stride : nullptr;
+    const unsigned ne = a.neras ? a.neras[k] : 0;
+    uint32_t *pos = a.positions ? a.positions + k * a.pos_stride : nullptr;
+    T *corr = a.corr ? static_cast<T *>(a.corr) + k * a.corr_stride : nullptr;
+    a.result[k] = decode_one<T, MAXR>(c, A, I, ID, FD, data, a.len, parity, eras, ne, pos, corr);
+}
+
+template <typename T, int MAXR>
+hipError_t enc_launch(const DevCodec &c, const EncodeArgs &a, hipStream_t s) {
+    const unsigned grid = (unsigned)((a.ncw + kBlock - 1) / kBlock);
+    if (c.nn <= 4095) {
+        const size_t sm = 2 * (c.nn + 1) * sizeof(uint16_t) + 512;
+        hipLaunchKernelGGL((k_encode_generic<T, MAXR, true>), dim3(grid), dim3(kBlock), sm, s, c, a);
+    } else {
+        hipLaunchKernelGGL((k_encode_generic<T, MAXR, false>), dim3(grid), dim3(kBlock), 0, s, c, a);
+    }
+    return hipGetLastError();
+}
+
+template <typename T, int MAXR>
+hipError_t dec_launch(const DevCodec &c, const DecodeArgs &a, hipStream_t s) {
+    const unsigned grid = (unsigned)((a.ncw + kBlock - 1) / kBlock);
+    if (c.nn <= 4095) {
+        const size_t sm = 2 * (c.nn + 1) * sizeof(uint16_t) + 512;
+        hipLaunchKernelGGL((k_decode_generic<T, MAXR, true>), dim3(grid), dim3(kBlock), sm, s, c, a);
+    } else {
+        hipLaunchKernelGGL((k_decode_generic<T, MAXR, false>), dim3(grid), dim3(kBlock), 0, s, c, a);
+    }
+    return hipGetLastError();
+}
+
+} // namespace
+
+hipError_t launch_encode_generic(const DevCodec &c, const EncodeArgs &a, hipStream_t s) {
+    if (a.ncw == 0) return hipSuccess;
+    if (c.mm <= 8) return c.nroots <= 32 ? enc_launch<uint8_t, 32>(c, a, s) : enc_launch<uint8_t, 256>(c, a, s);
+    return c.nroots <= 32 ? enc_launch<uint16_t, 32>(c, a, s) : enc_launch<uint16_t, 256>(c, a, s);
+}
+
+hipError_t launch_decode_generic(const DevCodec &c, const DecodeArgs &a, hipStream_t s) {
+    if (a.ncw == 0) return hipSuccess;
+    if (c.mm <= 8) return c.nroots <= 32 ? dec_launch<uint8_t, 32>(c, a, s) : dec_launch<uint8_t, 256>(c, a, s);
+    return c.nroots <= 32 ? dec_launch<uint16_t, 32>(c, a, s) : dec_launch<uint16_t, 256>(c, a, s);
+}
+
+} // namespace ezrs

@@ -1,0 +1,57 @@
+// ezrs_internal.hpp -- shared declarations of the MI355X RS engine (not part of the C ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <mutex>
+
+#include "ezrs_field.hpp"
+
+namespace ezrs {
+
+// Everything a kernel needs to know about a codec, passed by value at launch.
+struct DevCodec {
+    unsigned mm, nn, nroots, load, fcr, prim, iprim;
+    int dual;
+    int masked;                   // symbol narrower than its datum (rs_base:1194)
+    const uint16_t *alpha_to;     // device, nn+1
+    const uint16_t *index_of;     // device, nn+1
+    const uint16_t *genpoly;      // device, nroots+1 (index form)
+    const uint8_t *into_dual;     // device, 256
+    const uint8_t *from_dual;     // device, 256
+};
+
+// Arguments of one batch decode (strides in elements).
+struct DecodeArgs {
+    void *data;
+    size_t data_stride;
+    unsigned len;
+    void *parity;                 // never null here: the C ABI resolves parity == NULL
+    size_t parity_stride;
+    const uint32_t *eras;
+    size_t eras_stride;
+    const uint32_t *neras;
+    int32_t *result;
+    uint32_t *positions;
+    size_t pos_stride;
+    void *corr;
+    size_t corr_stride;
+    size_t ncw;
+};
+
+struct EncodeArgs {
+    const void *data;
+    size_t data_stride;
+    unsigned len;
+    void *parity;
+    size_t parity_stride;
+    size_t ncw;
+};
+
+// Generic per-codeword kernels (ezrs_generic.hip): every codec, every length.
+hipError_t launch_encode_generic(const DevCodec &c, const EncodeArgs &a, hipStream_t s);
+hipError_t launch_decode_generic(const DevCodec &c, const DecodeArgs &a, hipStream_t s);
+
+} // namespace ezrs

@@ -1,0 +1,202 @@
+"""Python host mirror of the MI355X RS engine (ctypes over lib/libezrs_hip.so, include/ezrs.h).
+
+Mirrors the reference's RS codec surface for the batch hot path:
+
+* ``Codec.rs(n, k)``          -- ezpwd::RS<N,K>                  (c++/ezpwd/rs:74-89)
+* ``Codec.ccsds(k, dual)``    -- ezpwd::RS_CCSDS[_CONV]<255,K>   (c++/ezpwd/rs:101-104)
+* ``Codec.encode(...)``       -- encode<TYP>(data, len, parity)  (c++/ezpwd/rs_base:868-904) per row
+* ``Codec.decode(...)``       -- decode<TYP>(data, len, parity, eras_pos, no_eras, corr)
+                                                                 (c++/ezpwd/rs_base:1170-1242) per row
+
+Device forms take torch tensors on the codec's device (PyTorch is only the allocator/stream
+provider here); host forms take numpy arrays and go through the library's pinned, double-buffered
+copy pipeline.  There is no CPU fallback: if the HIP library is missing or no GPU is visible,
+constructing a codec raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import errno
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libezrs_hip.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "ezrs.h")
+
+_vp, _sz, _u, _i = C.c_void_p, C.c_size_t, C.c_uint, C.c_int
+
+
+class EzrsError(RuntimeError):
+    pass
+
+
+class Info(C.Structure):
+    _fields_ = [("symbol_bits", _u), ("size", _u), ("nroots", _u), ("load", _u), ("poly", _u),
+                ("fcr", _u), ("prim", _u), ("datum_bytes", _u), ("dual", _i), ("device", _i)]
+
+
+_lib = None
+
+
+def lib():
+    """Load libezrs_hip.so; raise loudly if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise EzrsError(f"{LIB_PATH} is missing: build it with __graft_entry__.build() "
+                            "(make -C ezpwd-reed-solomon_amd/csrc)")
+        L = C.CDLL(LIB_PATH)
+        L.ezrs_abi_version.restype = _i
+        L.ezrs_device_count.restype = _i
+        L.ezrs_last_error.restype = C.c_char_p
+        L.ezrs_create.argtypes = [C.POINTER(_vp), _u, _u, _u, _u, _u, _i, _i]
+        L.ezrs_create_rs.argtypes = [C.POINTER(_vp), _u, _u, _i]
+        L.ezrs_create_ccsds.argtypes = [C.POINTER(_vp), _u, _i, _i]
+        L.ezrs_destroy.argtypes = [_vp]
+        L.ezrs_get_info.argtypes = [_vp, C.POINTER(Info)]
+        L.ezrs_reserve.argtypes = [_vp, _sz]
+        L.ezrs_encode.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _sz, _vp]
+        L.ezrs_decode.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _vp, _sz, _vp, _vp, _vp, _sz,
+                                  _vp, _sz, _sz, _vp]
+        L.ezrs_encode_host.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _sz, _sz]
+        L.ezrs_decode_host.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _vp, _sz, _vp, _vp, _vp,
+                                       _sz, _sz, _sz]
+        L.ezrs_host_alloc.argtypes = [C.POINTER(_vp), _sz]
+        L.ezrs_host_free.argtypes = [_vp]
+        _lib = L
+    return _lib
+
+
+def _check(rc, what):
+    if rc < 0:
+        msg = lib().ezrs_last_error().decode(errors="replace")
+        raise EzrsError(f"{what} failed: {errno.errorcode.get(-rc, rc)} {msg}")
+    return rc
+
+
+def _tp(t):
+    """Device pointer of a torch tensor (or None)."""
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _np(a):
+    return None if a is None else a.ctypes.data_as(_vp)
+
+
+def _stream_ptr(stream):
+    if stream is None:
+        import torch
+        stream = torch.cuda.current_stream()
+    return C.c_void_p(stream.cuda_stream) if hasattr(stream, "cuda_stream") else C.c_void_p(stream)
+
+
+class Codec:
+    """An RS(N,K) codec resident on one HIP device."""
+
+    def __init__(self, symbol_bits, poly, fcr, prim, nroots, dual=False, device=0, _h=None):
+        h = _vp()
+        if _h is None:
+            _check(lib().ezrs_create(C.byref(h), symbol_bits, poly, fcr, prim, nroots,
+                                     int(bool(dual)), device), "ezrs_create")
+        else:
+            h = _h
+        self._h = h
+        info = Info()
+        _check(lib().ezrs_get_info(self._h, C.byref(info)), "ezrs_get_info")
+        self.info = info
+        self.symbol_bits, self.nn, self.nroots, self.load = (info.symbol_bits, info.size,
+                                                             info.nroots, info.load)
+        self.dual, self.device = bool(info.dual), info.device
+        self.dtype = np.uint8 if info.datum_bytes == 1 else np.uint16
+
+    @classmethod
+    def rs(cls, n, k, device=0):
+        h = _vp()
+        _check(lib().ezrs_create_rs(C.byref(h), n, k, device), f"ezrs_create_rs({n},{k})")
+        return cls(0, 0, 0, 0, 0, _h=h)
+
+    @classmethod
+    def ccsds(cls, k, dual=True, device=0):
+        h = _vp()
+        _check(lib().ezrs_create_ccsds(C.byref(h), k, int(bool(dual)), device), "ezrs_create_ccsds")
+        return cls(0, 0, 0, 0, 0, _h=h)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            try:
+                lib().ezrs_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    def __repr__(self):
+        i = self.info
+        kind = ("RS_CCSDS" if i.dual else "RS_CCSDS_CONV") if i.poly == 0x187 else "RS"
+        return f"{kind}({i.size},{i.load})"
+
+    @property
+    def torch_dtype(self):
+        import torch
+        return torch.uint8 if self.dtype == np.uint8 else torch.uint16
+
+    def reserve(self, ncw):
+        _check(lib().ezrs_reserve(self._h, ncw), "ezrs_reserve")
+
+    # -- device batch forms ------------------------------------------------------------------
+    def encode(self, data, length=None, parity=None, stream=None):
+        """data: [ncw, stride] device tensor; parity: [ncw, >=nroots] or None (parity written
+        into columns length..length+nroots of data)."""
+        ncw, stride = data.shape
+        length = stride - self.nroots if length is None else length
+        ps = parity.stride(0) if parity is not None else 0
+        _check(lib().ezrs_encode(self._h, _tp(data), data.stride(0), length, _tp(parity), ps,
+                                 ncw, _stream_ptr(stream)), "ezrs_encode")
+
+    def decode(self, data, length=None, parity=None, eras=None, neras=None, result=None,
+               positions=None, corr=None, stream=None):
+        """In-place batch decode; returns the int32 result tensor."""
+        import torch
+        ncw, stride = data.shape
+        length = stride - self.nroots if length is None else length
+        if result is None:
+            result = torch.empty(ncw, dtype=torch.int32, device=data.device)
+        _check(lib().ezrs_decode(
+            self._h, _tp(data), data.stride(0), length, _tp(parity),
+            parity.stride(0) if parity is not None else 0,
+            _tp(eras), eras.stride(0) if eras is not None else 0, _tp(neras), _tp(result),
+            _tp(positions), positions.stride(0) if positions is not None else 0,
+            _tp(corr), corr.stride(0) if corr is not None else 0, ncw, _stream_ptr(stream)),
+            "ezrs_decode")
+        return result
+
+    # -- host batch forms ----------------------------------------------------------------------
+    def encode_host(self, data, length=None, parity=None, chunk=0):
+        ncw, stride = data.shape
+        length = stride - self.nroots if length is None else length
+        ps = parity.shape[1] if parity is not None else 0
+        _check(lib().ezrs_encode_host(self._h, _np(data), stride, length, _np(parity), ps, ncw,
+                                      chunk), "ezrs_encode_host")
+
+    def decode_host(self, data, length=None, parity=None, eras=None, neras=None,
+                    positions=None, chunk=0):
+        ncw, stride = data.shape
+        length = stride - self.nroots if length is None else length
+        result = np.zeros(ncw, np.int32)
+        _check(lib().ezrs_decode_host(
+            self._h, _np(data), stride, length, _np(parity),
+            parity.shape[1] if parity is not None else 0,
+            _np(eras), eras.shape[1] if eras is not None else 0, _np(neras), _np(result),
+            _np(positions), positions.shape[1] if positions is not None else 0, ncw, chunk),
+            "ezrs_decode_host")
+        return result
+
+
+def exported_symbols():
+    """Function names declared in include/ezrs.h."""
+    import re
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char \*|size_t)\s*\*?\s*(ezrs_\w+)\s*\(",
+                                 txt, re.M)))

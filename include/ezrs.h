@@ -1,0 +1,130 @@
+/*
+ * ezrs.h -- C ABI of the MI355X Reed-Solomon engine (libezrs_hip.so).
+ *
+ * Drop-in boundary for the hot path of pjkundert/ezpwd-reed-solomon: batched RS(N,K) encode and
+ * errors+erasures decode over GF(2^m), m = 2..16, bit-exact with the reference's
+ *
+ *   ezpwd::reed_solomon<...>::encode<INP>(data, len, parity)                 c++/ezpwd/rs_base:868-904
+ *   ezpwd::reed_solomon<...>::decode<INP>(data, len, parity, eras_pos,
+ *                                         no_eras, corr)                     c++/ezpwd/rs_base:1170-1242
+ *
+ * applied independently to every codeword of a batch.  The reference has no batch or C ABI for
+ * RS; each entry point below replaces a loop of those per-codeword calls (the loops in
+ * rsencode.C:93-163, exercise.H:121-199, rsvalidate.C:97-289).  Codec construction replaces the
+ * template instantiations ezpwd::RS<N,K>, RS_CCSDS<255,K>, RS_CCSDS_CONV<255,K> (c++/ezpwd/rs:74-104).
+ *
+ * Conventions
+ *   - All compute entry points take DEVICE pointers (hipMalloc'd, on the codec's device) and a
+ *     hipStream_t passed as void*; they are asynchronous and never allocate or synchronise once the
+ *     codec's workspace is reserved (ezrs_reserve), so they can be captured into a hipGraph.
+ *     ezrs_*_host take host pointers and run a chunked, double-buffered H2D/kernel/D2H pipeline.
+ *   - A codeword's symbols are stored as its datum type: uint8_t for m <= 8, uint16_t for m > 8
+ *     (the reference's TYP, rs:75-89).  Strides are in ELEMENTS of the respective array.
+ *   - `len` is the number of data (non-parity) symbols per codeword, 1..N-NROOTS; shorter codewords
+ *     are shortened codes with implicit leading zeros (rs_base:1302-1304, 1378).
+ *   - parity == NULL means the parity of each codeword immediately follows its data, at
+ *     data + len in the same row (the reference's decode(data, len+NROOTS) form, rs_base:1183-1186).
+ *   - Symbols narrower than their datum (e.g. RS(31,K) in uint8_t) follow the reference's masked
+ *     path: data bits above the symbol are ignored on encode and preserved on decode; a parity datum
+ *     with bits above the symbol fails that codeword's decode with -1 (rs_base:1194-1235).
+ *   - Return value of every function: 0 on success or a negative errno (-EINVAL bad arguments,
+ *     -ENODEV no usable HIP device, -ENOMEM, -EIO a HIP runtime error).  No C++ exception ever
+ *     crosses this ABI.  Per-codeword decode outcomes go to `result` (see ezrs_decode).
+ */
+#ifndef EZRS_H
+#define EZRS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EZRS_ABI_VERSION 1
+
+typedef struct ezrs_codec ezrs_codec;
+
+typedef struct ezrs_info {
+    unsigned symbol_bits;  /* m                                    (rs_base:570 SYMBOL/MM) */
+    unsigned size;         /* N = 2^m - 1                          (rs_base:571 SIZE/NN)   */
+    unsigned nroots;       /* N - K parity symbols                 (rs_base:723 NROOTS)    */
+    unsigned load;         /* K = N - NROOTS max data symbols      (rs_base:724 LOAD)      */
+    unsigned poly;         /* field polynomial                     (rs_base:756 poly())    */
+    unsigned fcr;          /* first consecutive root               (rs_base:762 fcr())     */
+    unsigned prim;         /* primitive element                    (rs_base:767 prim())    */
+    unsigned datum_bytes;  /* 1 (uint8_t) or 2 (uint16_t)          (rs_base:568 DATUM/8)   */
+    int dual;              /* CCSDS Berlekamp dual basis           (rs_base:772 dual())    */
+    int device;            /* HIP device the codec lives on */
+} ezrs_info;
+
+/* Library / device probe: returns the number of visible HIP devices (>= 0) or a negative errno. */
+int ezrs_device_count(void);
+/* ABI version of the loaded library (EZRS_ABI_VERSION). */
+int ezrs_abi_version(void);
+
+/* Generic codec over GF(2^m): replaces ezpwd::reed_solomon<TYP,SYM,RTS,FCR,PRM,gfpoly<SYM,PLY>,DUAL>
+ * (rs_base:702-1719).  Fails with -EINVAL where the reference's constructor would raise:
+ * non-primitive poly (rs_base:623-625), nroots == 0 or >= N (rs_base:1254-1256), dual with m != 8
+ * (rs_base:1188-1190). */
+int ezrs_create(ezrs_codec **out, unsigned symbol_bits, unsigned poly, unsigned fcr,
+                unsigned prim, unsigned nroots, int dual, int device);
+/* ezpwd::RS<N,K> -- the standard polynomial per N, FCR = 1, PRIM = 1 (rs:74-89). */
+int ezrs_create_rs(ezrs_codec **out, unsigned n, unsigned k, int device);
+/* ezpwd::RS_CCSDS<255,K> (dual = 1) / RS_CCSDS_CONV<255,K> (dual = 0): poly 0x187,
+ * FCR = 128 - (255-K)/2, PRIM = 11 (rs:101-104). */
+int ezrs_create_ccsds(ezrs_codec **out, unsigned k, int dual, int device);
+int ezrs_destroy(ezrs_codec *codec);
+int ezrs_get_info(const ezrs_codec *codec, ezrs_info *info);
+
+/* Pre-size the codec's device workspace for decode batches of up to `ncw` codewords, so that later
+ * ezrs_decode calls of that size neither allocate nor synchronise (graph-capture safe). */
+int ezrs_reserve(ezrs_codec *codec, size_t ncw);
+
+/* Batch encode -- for every codeword k < ncw:
+ *   encode<TYP>(data + k*data_stride, len, parity + k*parity_stride)          rs_base:868-904
+ * data and parity are device arrays of the datum type. */
+int ezrs_encode(const ezrs_codec *codec, const void *data, size_t data_stride, unsigned len,
+                void *parity, size_t parity_stride, size_t ncw, void *stream);
+
+/* Batch decode -- for every codeword k < ncw, in place:
+ *   result[k] = decode<TYP>(data + k*data_stride, len, parity + k*parity_stride,
+ *                           eras_pos_k, neras[k], corr + k*corr_stride)      rs_base:1170-1242
+ * eras       (nullable) uint32 rows of eras_stride entries: erasure positions relative to data[0]
+ *            (parity positions follow at len..len+NROOTS-1); neras (nullable) their counts.
+ * result     int32[ncw]: number of corrected symbols (erasures included, even when the erased
+ *            symbol was already right), 0 for a valid codeword, -1 if uncorrectable or invalid
+ *            (rs_base:1335-1718).  On -1 the direct (unmasked) path may leave partial
+ *            corrections applied, exactly as the reference does (rs_base:1610-1690, 1238-1241).
+ * positions  (nullable) uint32 rows of pos_stride >= NROOTS: entries 0..result[k]-1 receive the
+ *            corrected positions relative to data[0], in the reference's Chien-search order
+ *            (rs_base:1557-1576, 1713-1716); other entries are left untouched.
+ * corr       (nullable) datum rows of corr_stride >= NROOTS: corr[j] receives the correction
+ *            pattern of position j, for the j the reference writes (rs_base:1658-1687). */
+int ezrs_decode(const ezrs_codec *codec, void *data, size_t data_stride, unsigned len,
+                void *parity, size_t parity_stride, const uint32_t *eras, size_t eras_stride,
+                const uint32_t *neras, int32_t *result, uint32_t *positions, size_t pos_stride,
+                void *corr, size_t corr_stride, size_t ncw, void *stream);
+
+/* Host-memory forms: the same contracts with HOST pointers.  The batch is streamed through the
+ * device in chunks of `chunk` codewords (0 = library default) over two HIP streams with
+ * asynchronous copies; pinned host memory (ezrs_host_alloc) gets full PCIe overlap.  Blocking:
+ * they return when the results are back in host memory. */
+int ezrs_encode_host(ezrs_codec *codec, const void *data, size_t data_stride, unsigned len,
+                     void *parity, size_t parity_stride, size_t ncw, size_t chunk);
+int ezrs_decode_host(ezrs_codec *codec, void *data, size_t data_stride, unsigned len,
+                     void *parity, size_t parity_stride, const uint32_t *eras,
+                     size_t eras_stride, const uint32_t *neras, int32_t *result,
+                     uint32_t *positions, size_t pos_stride, size_t ncw, size_t chunk);
+
+/* Pinned host memory for the host-memory forms (hipHostMalloc / hipHostFree). */
+int ezrs_host_alloc(void **ptr, size_t bytes);
+int ezrs_host_free(void *ptr);
+
+/* Human-readable text of the last HIP error seen by this thread ("" if none). */
+const char *ezrs_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EZRS_H */

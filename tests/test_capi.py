@@ -1,0 +1,55 @@
+"""CPU tests of the drop-in boundary: the C-ABI library loads, exports every function that
+include/ezrs.h declares, and rejects invalid codecs without touching a GPU."""
+import ctypes as C
+import errno
+import os
+import subprocess
+
+import pytest
+
+import ezrs
+
+
+def test_library_exports_every_declared_symbol():
+    L = ezrs.lib()
+    declared = ezrs.exported_symbols()
+    assert len(declared) >= 15
+    for name in declared:
+        assert hasattr(L, name), name
+    out = subprocess.check_output(["nm", "-D", "--defined-only", ezrs.LIB_PATH], text=True)
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    assert set(declared) <= exported
+
+
+def test_abi_version():
+    assert ezrs.lib().ezrs_abi_version() == 1
+
+
+def test_invalid_codecs_rejected_before_device():
+    L = ezrs.lib()
+    h = C.c_void_p()
+    assert L.ezrs_create(C.byref(h), 8, 0x11d, 1, 1, 0, 0, 0) == -errno.EINVAL
+    assert L.ezrs_create(C.byref(h), 8, 0x101, 1, 1, 32, 0, 0) == -errno.EINVAL
+    assert L.ezrs_create(C.byref(h), 10, 0x409, 1, 1, 32, 1, 0) == -errno.EINVAL
+    assert L.ezrs_create_rs(C.byref(h), 256, 223, 0) == -errno.EINVAL
+    assert L.ezrs_create_ccsds(C.byref(h), 224, 1, 0) == -errno.EINVAL
+    assert not h.value
+
+
+def test_null_codec_calls_are_einval():
+    L = ezrs.lib()
+    assert L.ezrs_encode(None, None, 0, 1, None, 0, 1, None) == -errno.EINVAL
+    assert L.ezrs_decode(None, None, 0, 1, None, 0, None, 0, None, None, None, 0, None, 0, 1,
+                         None) == -errno.EINVAL
+    assert L.ezrs_destroy(None) == 0
+
+
+@pytest.mark.skipif(os.environ.get("HIP_VISIBLE_DEVICES") is None and
+                    os.path.exists("/dev/kfd"), reason="a GPU is visible here")
+def test_no_device_reports_enodev():
+    L = ezrs.lib()
+    h = C.c_void_p()
+    rc = L.ezrs_create_rs(C.byref(h), 255, 223, 0)
+    assert rc == -errno.ENODEV
+    with pytest.raises(ezrs.EzrsError):
+        ezrs.Codec.rs(255, 223)

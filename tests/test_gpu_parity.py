@@ -1,0 +1,187 @@
+"""GPU parity tests: the HIP engine through the C ABI against the reference's golden vectors and
+the oracle (CPU restatement) on identical seeded inputs.  Bit-exact equality everywhere."""
+import numpy as np
+import pytest
+
+import oracle as O
+from golden_util import fixture_files, fixture_id, load
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as T
+    if not T.cuda.is_available():
+        pytest.skip("no GPU")
+    return T
+
+
+def _codec(params):
+    import ezrs
+    mm, poly, fcr, prim, nroots, dual = (int(x) for x in params)
+    return ezrs.Codec(mm, poly, fcr, prim, nroots, bool(dual))
+
+
+def _tdt(torch, dt):
+    return torch.uint8 if dt == np.uint8 else torch.uint16
+
+
+def _to_dev(torch, a):
+    if a.dtype == np.uint16:
+        return torch.from_numpy(a.view(np.int16)).view(torch.uint16).cuda()
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def _to_np(t, dt):
+    t = t.cpu()
+    if dt == np.uint16:
+        return t.view(__import__("torch").int16).numpy().view(np.uint16)
+    return t.numpy()
+
+
+@pytest.mark.parametrize("fn", fixture_files(), ids=fixture_id)
+def test_golden_device(torch, fn):
+    f = load(fn)
+    c = _codec(f["params"])
+    dt = c.dtype
+    nr = c.nroots
+    for t in range(len(f["length"])):
+        L = int(f["length"][t])
+        d = _to_dev(torch, f["enc_data"][t:t + 1, :L].copy())
+        p = torch.zeros((1, nr), dtype=_tdt(torch, dt), device="cuda")
+        c.encode(d, L, p)
+        np.testing.assert_array_equal(_to_np(p, dt)[0], f["enc_parity"][t], err_msg=f"enc t={t}")
+
+        d = _to_dev(torch, f["dec_data_in"][t:t + 1, :L].copy())
+        p = _to_dev(torch, f["dec_parity_in"][t:t + 1].copy())
+        corr = _to_dev(torch, f["dec_corr_in"][t:t + 1].copy())
+        ne = int(f["dec_neras"][t])
+        eras = torch.from_numpy(f["dec_eras"][t:t + 1].astype(np.int32)).cuda()
+        neras = torch.tensor([ne], dtype=torch.int32, device="cuda")
+        pos = torch.zeros((1, max(nr, 1)), dtype=torch.int32, device="cuda")
+        r = c.decode(d, L, p, eras=eras, neras=neras, positions=pos, corr=corr)
+        torch.cuda.synchronize()
+        res = int(r.cpu()[0])
+        assert res == f["dec_result"][t], f"t={t}"
+        np.testing.assert_array_equal(pos.cpu().numpy()[0, :max(res, 0)].astype(np.uint32),
+                                      f["dec_positions"][t, :max(res, 0)])
+        np.testing.assert_array_equal(_to_np(d, dt)[0], f["dec_data_out"][t, :L])
+        np.testing.assert_array_equal(_to_np(p, dt)[0], f["dec_parity_out"][t])
+        np.testing.assert_array_equal(_to_np(corr, dt)[0], f["dec_corr_out"][t])
+
+
+@pytest.mark.parametrize("fn", fixture_files()[::3], ids=fixture_id)
+def test_golden_host_pipeline(torch, fn):
+    f = load(fn)
+    c = _codec(f["params"])
+    nr = c.nroots
+    for t in range(len(f["length"])):
+        L = int(f["length"][t])
+        d = f["enc_data"][t:t + 1, :L].copy()
+        p = np.zeros((1, nr), c.dtype)
+        c.encode_host(d, L, p)
+        np.testing.assert_array_equal(p[0], f["enc_parity"][t])
+        d = f["dec_data_in"][t:t + 1, :L].copy()
+        p = f["dec_parity_in"][t:t + 1].copy()
+        ne = int(f["dec_neras"][t])
+        eras = f["dec_eras"][t:t + 1].copy()
+        neras = np.array([ne], np.uint32)
+        pos = np.zeros((1, nr), np.uint32)
+        r = c.decode_host(d, L, p, eras=eras, neras=neras, positions=pos)
+        assert r[0] == f["dec_result"][t]
+        np.testing.assert_array_equal(pos[0, :max(r[0], 0)], f["dec_positions"][t, :max(r[0], 0)])
+        np.testing.assert_array_equal(d[0], f["dec_data_out"][t, :L])
+        np.testing.assert_array_equal(p[0], f["dec_parity_out"][t])
+
+
+def _inject(torch, cw, n_err, n_era, nn, gen):
+    """Corrupt n_err + n_era distinct symbols per row; the last n_era are flagged as erasures."""
+    ncw, n = cw.shape
+    keys = torch.rand((ncw, n), generator=gen, device=cw.device)
+    locs = keys.argsort(dim=1)[:, :n_err + n_era]
+    vals = torch.randint(1, nn + 1, (ncw, n_err + n_era), generator=gen, device=cw.device,
+                         dtype=torch.int32).to(cw.dtype)
+    cw.scatter_(1, locs, cw.gather(1, locs) ^ vals)
+    eras = locs[:, n_err:].to(torch.int32).contiguous()
+    return locs, eras
+
+
+@pytest.mark.parametrize("maker", ["RS(255,223)", "RS_CCSDS(255,223)", "RS(255,251)"])
+def test_bulk_vs_oracle(torch, maker):
+    """64k codewords, random shortened length, error loads 0..3x capacity: every output equals
+    the oracle's (result, positions, corrected data and parity)."""
+    import ezrs
+    c = ezrs.Codec.rs(255, int(maker[7:-1])) if maker.startswith("RS(") else ezrs.Codec.ccsds(223)
+    oc = O.Codec(*(O.rs_params(255, c.load) if maker.startswith("RS(") else O.ccsds_params(223)))
+    rng = np.random.default_rng(11)
+    ncw, L, nr = 1 << 16, c.load - 17, c.nroots
+    data = rng.integers(0, 256, (ncw, L + nr)).astype(np.uint8)
+    ref = data.copy()
+    oc.encode_batch(ref, L, None, nthreads=8)
+    dev = torch.from_numpy(data).cuda()
+    c.encode(dev, L)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(dev.cpu().numpy(), ref)
+    # corrupt the oracle's codewords with varying loads
+    load = rng.integers(0, 3 * nr // 2 + 1, ncw)
+    cw = ref.copy()
+    eras = np.zeros((ncw, nr), np.uint32)
+    neras = np.zeros(ncw, np.uint32)
+    for k in range(ncw):
+        m = int(load[k])
+        locs = rng.choice(L + nr, m, replace=False)
+        cw[k, locs] ^= rng.integers(1, 256, m).astype(np.uint8)
+        ne = min(int(rng.integers(0, m + 1)), nr)
+        eras[k, :ne] = locs[:ne]
+        neras[k] = ne
+    exp = cw.copy()
+    exp_pos = np.zeros((ncw, nr), np.uint32)
+    exp_r = oc.decode_batch(exp, L, None, eras, neras, exp_pos, nthreads=8)
+    dcw = torch.from_numpy(cw).cuda()
+    pos = torch.zeros((ncw, nr), dtype=torch.int32, device="cuda")
+    r = c.decode(dcw, L, None, eras=torch.from_numpy(eras.view(np.int32)).cuda(),
+                 neras=torch.from_numpy(neras.view(np.int32)).cuda(), positions=pos)
+    torch.cuda.synchronize()
+    r = r.cpu().numpy()
+    np.testing.assert_array_equal(r, exp_r)
+    np.testing.assert_array_equal(dcw.cpu().numpy(), exp)
+    pos = pos.cpu().numpy().view(np.uint32)
+    for k in np.nonzero(r > 0)[0]:
+        np.testing.assert_array_equal(pos[k, :r[k]], exp_pos[k, :r[k]])
+    assert (r == -1).any() and (r == 0).any() and (r > 0).any()
+
+
+def test_c2_c3_full_size(torch):
+    """BASELINE configs C2/C3 at full size (1M RS(255,223) codewords): encode parity equals the
+    oracle on a sample; clean decode returns 0 everywhere; 8 errors + 4 erasures per codeword
+    decode to result 12 with the original codewords restored (size-independent properties)."""
+    import ezrs
+    c = ezrs.Codec.rs(255, 223)
+    oc = O.Codec(*O.rs_params(255, 223))
+    ncw = 1 << 20
+    gen = torch.Generator(device="cuda").manual_seed(0x5EED0002)
+    cw = torch.randint(0, 256, (ncw, 255), generator=gen, device="cuda", dtype=torch.int32)
+    cw = cw.to(torch.uint8)
+    c.encode(cw, 223)
+    torch.cuda.synchronize()
+    host = cw.cpu().numpy()
+    sample = host[::61].copy()
+    exp = sample.copy()
+    oc.encode_batch(exp, 223, None, nthreads=8)
+    np.testing.assert_array_equal(sample, exp)
+    clean = cw.clone()
+    r = c.decode(clean, 223)
+    torch.cuda.synchronize()
+    assert int((r != 0).sum()) == 0
+    assert torch.equal(clean, cw)
+    bad = cw.clone()
+    locs, eras = _inject(torch, bad, 8, 4, 255, gen)
+    neras = torch.full((ncw,), 4, dtype=torch.int32, device="cuda")
+    pos = torch.zeros((ncw, 32), dtype=torch.int32, device="cuda")
+    r = c.decode(bad, 223, eras=eras, neras=neras, positions=pos)
+    torch.cuda.synchronize()
+    assert int((r != 12).sum()) == 0
+    assert torch.equal(bad, cw)
+    exp_pos = locs.sort(dim=1).values.to(torch.int32)       # PRIM = 1: ascending order
+    assert torch.equal(pos[:, :12], exp_pos)
