@@ -1,0 +1,204 @@
+#!/usr/bin/env python3
+"""Generate the constant tables of the bit-sliced GF(2^8) RS kernels (csrc/gen/ezrs_bs_tables.inc).
+
+The kernels evaluate syndromes S_i = r(g_i), g_i = alpha^((fcr+i)*prim) (c++/ezpwd/rs_base:1390-1414),
+on 32 slots per 32-bit register: 8 codewords x 4 interleaved segments (positions p = 4y + s).
+Per segment, Horner in d_i = g_i^4 runs in blocks of 16 y-steps:
+
+    G_i <- G_i * d_i^16 + sum_{t<16} c_{4(16k+t)+s} * d_i^(15-t)
+
+and the segments are folded with  S_i = g_i^2 (g_i G_0 + G_1) + (g_i G_2 + G_3).  Every constant
+multiplication is a GF(2)-linear 8x8 bit map; the tables below give, for every output bit, the
+4-bit masks of input bits 0-3 and 4-7 it XORs (the kernels precompute all 15 XOR-combinations of
+each input nibble once and spend one v_bitop3 per output bit and input byte).
+
+Encode evaluates the data word only and maps the syndromes to parity with the GF(2) matrix Q of
+parity = into_dual?( V^-1 (g^NR * H(data)) ) (see gf8.Codec8.q_rows); its table QN gives, per
+output bit and input syndrome, the (lo, hi) nibble masks.
+
+Dual-basis codecs fold from_dual into every input map and into_dual into Q, so the kernels never
+touch the dual-basis tables (rs_base:109-146, 1312, 1324-1326).
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+from gf8 import Codec8  # noqa: E402
+
+# (name, poly, fcr, prim, nroots, dual) -- the codecs with a bit-sliced fast path
+CODECS = [
+    ("RS_255_223", 0x11d, 1, 1, 32, False),
+    ("RS_255_239", 0x11d, 1, 1, 16, False),
+    ("RS_255_251", 0x11d, 1, 1, 4, False),
+    ("CCSDS_255_223", 0x187, 112, 11, 32, True),
+    ("CCSDS_CONV_255_223", 0x187, 112, 11, 32, False),
+]
+
+NROLES = 2
+BLOCK = 16     # y-steps per block (one LDS chunk = 64 positions)
+
+
+def split(nr):
+    h = (nr + 1) // 2
+    return [(0, h), (h, nr - h)]
+
+
+def nib(row):
+    return (row & 15) | ((row >> 4) & 15) << 4
+
+
+def fmt(arr, depth=0):
+    if isinstance(arr, list):
+        return "{" + ",".join(fmt(a, depth + 1) for a in arr) + "}"
+    return str(arr)
+
+
+def emit_combos(out, name, srcs, ind):
+    a = srcs
+    out.append(f"{ind}const uint32_t {name}1 = {a[0]}, {name}2 = {a[1]}, {name}4 = {a[2]}, {name}8 = {a[3]};")
+    out.append(f"{ind}const uint32_t {name}3 = {name}1 ^ {name}2, {name}5 = {name}1 ^ {name}4, "
+               f"{name}6 = {name}2 ^ {name}4, {name}9 = {name}1 ^ {name}8, {name}10 = {name}2 ^ {name}8, "
+               f"{name}12 = {name}4 ^ {name}8;")
+    out.append(f"{ind}const uint32_t {name}7 = {name}3 ^ {name}4, {name}11 = {name}3 ^ {name}8, "
+               f"{name}13 = {name}5 ^ {name}8, {name}14 = {name}6 ^ {name}8;")
+    out.append(f"{ind}const uint32_t {name}15 = {name}7 ^ {name}8;")
+    out.append(f"{ind}(void){name}1; (void){name}2; (void){name}3; (void){name}4; (void){name}5; "
+               f"(void){name}6; (void){name}7; (void){name}8; (void){name}9; (void){name}10; "
+               f"(void){name}11; (void){name}12; (void){name}13; (void){name}14; (void){name}15;")
+
+
+def upd(dst, acc, m, lo="l", hi="h"):
+    ml, mh = m & 15, m >> 4
+    terms = ([f"{lo}{ml}"] if ml else []) + ([f"{hi}{mh}"] if mh else [])
+    if acc is None:
+        if not terms:
+            return f"{dst} = 0u;"
+        if len(terms) == 1:
+            return f"{dst} = {terms[0]};"
+        return f"{dst} = {terms[0]} ^ {terms[1]};"
+    if not terms:
+        return None
+    if len(terms) == 1:
+        return f"{dst} ^= {terms[0]};"
+    return f"{dst} = xor3({acc}, {terms[0]}, {terms[1]});"
+
+
+def gen_codec(name, poly, fcr, prim, nr, dual):
+    C = Codec8(poly, fcr, prim, nr, dual)
+    gf = C.gf
+    roles = split(nr)
+    Q = C.q_rows()
+    st = f"BS_{name}"
+    out = [f"struct {st} {{",
+           f"    static constexpr unsigned POLY = {poly:#x}, FCR = {fcr}, PRIM = {prim}, NR = {nr};",
+           f"    static constexpr bool DUAL = {'true' if dual else 'false'};",
+           f"    static constexpr int S0[2] = {{{roles[0][0]}, {roles[1][0]}}};",
+           f"    static constexpr int NS[2] = {{{roles[0][1]}, {roles[1][1]}}};",
+           "    template <int R> static __device__ void horner_chunk(uint32_t (&S)[16][8], "
+           "const uint32_t *tile, int lane, bool first);",
+           "    template <int R> static __device__ void fold(uint32_t (&S)[16][8]);",
+           "    template <int R> static __device__ void parity_map(uint32_t (&S)[16][8], "
+           "const uint32_t *qin, int lane);",
+           "};"]
+    for r, (r0, n) in enumerate(roles):
+        I = "    "
+        # ---- Horner chunk
+        out.append(f"template <> __device__ __forceinline__ void {st}::horner_chunk<{r}>("
+                   "uint32_t (&S)[16][8], const uint32_t *tile, int lane, bool first) {")
+        out.append(f"{I}if (!first) {{")
+        for i in range(n):
+            rows = C.mul_rows(gf.pow(gf.pow(C.roots[r0 + i], 4), BLOCK))
+            out.append(f"{I}    {{")
+            emit_combos(out, "l", [f"S[{i}][{q}]" for q in range(4)], I + "        ")
+            emit_combos(out, "h", [f"S[{i}][{q}]" for q in range(4, 8)], I + "        ")
+            for q in range(8):
+                out.append(f"{I}        " + upd(f"S[{i}][{q}]", None, nib(rows[q])))
+            out.append(f"{I}        __builtin_amdgcn_sched_barrier(0);")
+            out.append(f"{I}    }}")
+        out.append(f"{I}}}")
+        for t in range(BLOCK):
+            out.append(f"{I}{{ // y-step {t}")
+            out.append(f"{I}    uint32_t P[8];")
+            out.append(f"{I}    #pragma unroll")
+            out.append(f"{I}    for (int b = 0; b < 8; ++b) P[b] = tile[(lane + 64 * b) * 17 + {t}];")
+            emit_combos(out, "l", ["P[0]", "P[1]", "P[2]", "P[3]"], I + "    ")
+            emit_combos(out, "h", ["P[4]", "P[5]", "P[6]", "P[7]"], I + "    ")
+            for i in range(n):
+                d = gf.pow(C.roots[r0 + i], 4)
+                rows = C.input_rows(gf.pow(d, BLOCK - 1 - t))
+                for q in range(8):
+                    ln = upd(f"S[{i}][{q}]", f"S[{i}][{q}]", nib(rows[q]))
+                    if ln:
+                        out.append(f"{I}    " + ln)
+            out.append(f"{I}    __builtin_amdgcn_sched_barrier(0);")
+            out.append(f"{I}}}")
+        out.append("}")
+        # ---- segment fold
+        out.append(f"template <> __device__ __forceinline__ void {st}::fold<{r}>(uint32_t (&S)[16][8]) {{")
+        for lvl, sh in ((1, 8), (2, 16)):
+            for i in range(n):
+                g = C.roots[r0 + i]
+                rows = C.mul_rows(g if lvl == 1 else gf.mul(g, g))
+                out.append(f"{I}{{")
+                emit_combos(out, "l", [f"(S[{i}][{q}] << {sh})" for q in range(4)], I + "    ")
+                emit_combos(out, "h", [f"(S[{i}][{q}] << {sh})" for q in range(4, 8)], I + "    ")
+                for q in range(8):
+                    ln = upd(f"S[{i}][{q}]", f"S[{i}][{q}]", nib(rows[q]))
+                    if ln:
+                        out.append(f"{I}    " + ln)
+                out.append(f"{I}    __builtin_amdgcn_sched_barrier(0);")
+                out.append(f"{I}}}")
+        out.append("}")
+        # ---- encode parity map
+        out.append(f"template <> __device__ __forceinline__ void {st}::parity_map<{r}>("
+                   "uint32_t (&S)[16][8], const uint32_t *qin, int lane) {")
+        first = [[True] * 8 for _ in range(n)]
+        for i in range(nr):
+            out.append(f"{I}{{ // syndrome {i}")
+            out.append(f"{I}    const uint32_t w0 = qin[lane * 65 + {2 * i}], w1 = qin[lane * 65 + {2 * i + 1}];")
+            emit_combos(out, "l", ["(w0 << 24)", "(w0 << 16)", "(w0 << 8)", "w0"], I + "    ")
+            emit_combos(out, "h", ["(w1 << 24)", "(w1 << 16)", "(w1 << 8)", "w1"], I + "    ")
+            for jl in range(n):
+                for b in range(8):
+                    row = Q[8 * (r0 + jl) + b]
+                    m = nib((row >> (8 * i)) & 0xFF)
+                    if first[jl][b]:
+                        out.append(f"{I}    " + upd(f"S[{jl}][{b}]", None, m))
+                        first[jl][b] = False
+                    else:
+                        ln = upd(f"S[{jl}][{b}]", f"S[{jl}][{b}]", m)
+                        if ln:
+                            out.append(f"{I}    " + ln)
+            out.append(f"{I}    __builtin_amdgcn_sched_barrier(0);")
+            out.append(f"{I}}}")
+        out.append("}")
+    return "\n".join(out)
+
+
+def main(dst=None):
+    dst = dst or os.path.join(HERE, "..", "csrc", "gen", "ezrs_bs_tables.inc")
+    os.makedirs(os.path.dirname(dst), exist_ok=True)
+    body = ["// GENERATED by codegen/gen_bitslice.py -- do not edit.",
+            "// Straight-line XOR networks of the bit-sliced GF(2^8) RS kernels (see ezrs_bitslice.hip).",
+            "#pragma once", "#include <cstdint>", "namespace ezrs { namespace bs {",
+            "__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {",
+            "    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);", "}"]
+    for c in CODECS:
+        body.append(gen_codec(*c))
+    body.append("#define EZRS_BS_CODEC_LIST(X) \\")
+    for i, (name, poly, fcr, prim, nr, dual) in enumerate(CODECS):
+        sep = " \\" if i + 1 < len(CODECS) else ""
+        body.append(f"    X(BS_{name}){sep}")
+    body.append("} } // namespace ezrs::bs")
+    txt = "\n".join(body) + "\n"
+    old = open(dst).read() if os.path.exists(dst) else None
+    if old != txt:
+        with open(dst, "w") as f:
+            f.write(txt)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else None)

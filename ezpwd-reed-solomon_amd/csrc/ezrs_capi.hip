@@ -27,6 +27,9 @@ struct ezrs_codec {
     void *d_stage[2] = {nullptr, nullptr};
     size_t stage_bytes = 0;
     hipStream_t streams[2] = {nullptr, nullptr};
+    int bs_id = -1;               // bit-sliced GF(2^8) kernel set, -1 if none
+    uint8_t *d_syn = nullptr;     // decode workspace: syndromes of flagged codewords, [ncw][32]
+    size_t syn_cap = 0;           // codewords the workspace can hold
 };
 
 namespace {
@@ -123,12 +126,14 @@ int ezrs_create(ezrs_codec **out, unsigned symbol_bits, unsigned poly, unsigned 
     DevCodec &d = c->dev;
     d.mm = m.spec.mm; d.nn = m.nn; d.nroots = m.spec.nroots; d.load = m.load;
     d.fcr = m.spec.fcr; d.prim = m.spec.prim; d.iprim = m.iprim; d.dual = m.spec.dual;
+    d.poly = m.spec.poly;
     d.masked = m.spec.mm != (m.spec.mm <= 8 ? 8u : 16u);
     d.alpha_to = c->d_tabs;
     d.index_of = c->d_tabs + (m.nn + 1);
     d.genpoly = c->d_tabs + 2 * (m.nn + 1);
     d.into_dual = c->d_dual;
     d.from_dual = c->d_dual + 256;
+    c->bs_id = bitslice_codec_id(d);
     *out = c;
     return 0;
 }
@@ -158,6 +163,7 @@ int ezrs_destroy(ezrs_codec *c) {
     DeviceGuard g(c->device);
     (void)hipFree(c->d_tabs);
     (void)hipFree(c->d_dual);
+    if (c->d_syn) (void)hipFree(c->d_syn);
     for (int i = 0; i < 2; ++i) {
         if (c->d_stage[i]) (void)hipFree(c->d_stage[i]);
         if (c->h_stage[i]) (void)hipHostFree(c->h_stage[i]);
@@ -183,10 +189,28 @@ int ezrs_get_info(const ezrs_codec *c, ezrs_info *info) {
     return 0;
 }
 
+namespace {
+
+// Grow the flagged-codeword syndrome workspace (bit-sliced decode path only).
+int reserve_syn(ezrs_codec *c, size_t ncw) {
+    if (c->bs_id < 0 || ncw <= c->syn_cap) return 0;
+    DeviceGuard g(c->device);
+    if (c->d_syn) {
+        HIP_TRY(hipDeviceSynchronize());
+        (void)hipFree(c->d_syn);
+        c->d_syn = nullptr;
+        c->syn_cap = 0;
+    }
+    HIP_TRY(hipMalloc(&c->d_syn, ncw * 32));
+    c->syn_cap = ncw;
+    return 0;
+}
+
+} // namespace
+
 int ezrs_reserve(ezrs_codec *c, size_t ncw) {
     if (!c) return -EINVAL;
-    (void)ncw;  // the generic path needs no workspace
-    return 0;
+    return reserve_syn(c, ncw);
 }
 
 int ezrs_encode(const ezrs_codec *c, const void *data, size_t data_stride, unsigned len,
@@ -206,7 +230,8 @@ int ezrs_encode(const ezrs_codec *c, const void *data, size_t data_stride, unsig
     if (ncw > 1 && data_stride < len) return -EINVAL;
     DeviceGuard g(c->device);
     EncodeArgs a{data, data_stride, len, parity, parity_stride, ncw};
-    hipError_t e = launch_encode_generic(c->dev, a, static_cast<hipStream_t>(stream));
+    hipError_t e = c->bs_id >= 0 ? launch_bs_encode(c->bs_id, a, static_cast<hipStream_t>(stream))
+                                 : launch_encode_generic(c->dev, a, static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return hip_fail(e, "encode launch");
     return 0;
 }
@@ -235,7 +260,19 @@ int ezrs_decode(const ezrs_codec *c, void *data, size_t data_stride, unsigned le
     DeviceGuard g(c->device);
     DecodeArgs a{data, data_stride, len, parity, parity_stride, eras, eras_stride, neras,
                  result, positions, pos_stride, corr, corr_stride, ncw};
-    hipError_t e = launch_decode_generic(c->dev, a, static_cast<hipStream_t>(stream));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const bool contiguous =
+        parity == static_cast<char *>(data) + (size_t)len * w && parity_stride == data_stride;
+    hipError_t e;
+    if (c->bs_id >= 0 && contiguous) {
+        // Bit-sliced syndromes for the whole batch; the reference algorithm only for the codewords
+        // that are not valid as received (or carry erasures to validate).
+        if (int r = reserve_syn(const_cast<ezrs_codec *>(c), ncw)) return r;
+        e = launch_bs_syndromes(c->bs_id, c->dev, a, c->d_syn, st);
+        if (e == hipSuccess) e = launch_decode_flagged(c->dev, a, c->d_syn, st);
+    } else {
+        e = launch_decode_generic(c->dev, a, st);
+    }
     if (e != hipSuccess) return hip_fail(e, "decode launch");
     return 0;
 }

@@ -101,7 +101,8 @@ template <typename T, int MAXR>
 __device__ int decode_one(const DevCodec &c, const uint16_t *__restrict__ A,
                           const uint16_t *__restrict__ I, const uint8_t *ID, const uint8_t *FD,
                           T *data, unsigned len, T *parity, const uint32_t *eras,
-                          unsigned no_eras, uint32_t *pos_out, T *corr_out) {
+                          unsigned no_eras, uint32_t *pos_out, T *corr_out,
+                          const uint8_t *syn_in = nullptr) {
     const unsigned NR = c.nroots, NN = c.nn, A0 = c.nn, mm = c.mm, LOAD = c.load;
     const unsigned FCR = c.fcr, PRM = c.prim;
     if (len == 0 || len > LOAD) return -1;                                    // 1375-1377
@@ -125,8 +126,11 @@ __device__ int decode_one(const DevCodec &c, const uint16_t *__restrict__ A,
         x &= NN;
         return c.dual ? FD[x] : x;
     };
-    // syndromes by Horner over data then parity (1390-1414)
-    {
+    // syndromes by Horner over data then parity (1390-1414), unless the bit-sliced kernel
+    // already evaluated them (same values: S_i = r(alpha^((fcr+i)*prim)) in polynomial form)
+    if (syn_in) {
+        for (unsigned i = 0; i < NR; ++i) syn[i] = syn_in[i];
+    } else {
         const unsigned s0 = cnv(data[0]);
         for (unsigned i = 0; i < NR; ++i) syn[i] = (uint16_t)s0;
         for (unsigned j = 1; j < len + NR; ++j) {
@@ -291,6 +295,26 @@ __global__ void __launch_bounds__(kBlock) k_decode_generic(DevCodec c, DecodeArg
     a.result[k] = decode_one<T, MAXR>(c, A, I, ID, FD, data, a.len, parity, eras, ne, pos, corr);
 }
 
+constexpr int32_t kSentinel = INT32_MIN;
+
+__global__ void __launch_bounds__(kBlock) k_decode_flagged(DevCodec c, DecodeArgs a,
+                                                           const uint8_t *syn_ws) {
+    __shared__ __attribute__((aligned(16))) uint16_t smem[2 * 256 + 256];
+    const uint16_t *A, *I;
+    const uint8_t *ID, *FD;
+    stage_tables<true>(c, smem, A, I, ID, FD);
+    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= a.ncw || a.result[k] != kSentinel) return;
+    uint8_t *data = static_cast<uint8_t *>(a.data) + k * a.data_stride;
+    uint8_t *parity = static_cast<uint8_t *>(a.parity) + k * a.parity_stride;
+    const uint32_t *eras = a.eras ? a.eras + k * a.eras_stride : nullptr;
+    const unsigned ne = a.neras ? a.neras[k] : 0;
+    uint32_t *pos = a.positions ? a.positions + k * a.pos_stride : nullptr;
+    uint8_t *corr = a.corr ? static_cast<uint8_t *>(a.corr) + k * a.corr_stride : nullptr;
+    a.result[k] = decode_one<uint8_t, 32>(c, A, I, ID, FD, data, a.len, parity, eras, ne, pos,
+                                          corr, syn_ws + k * 32);
+}
+
 template <typename T, int MAXR>
 hipError_t enc_launch(const DevCodec &c, const EncodeArgs &a, hipStream_t s) {
     const unsigned grid = (unsigned)((a.ncw + kBlock - 1) / kBlock);
@@ -316,6 +340,14 @@ hipError_t dec_launch(const DevCodec &c, const DecodeArgs &a, hipStream_t s) {
 }
 
 } // namespace
+
+hipError_t launch_decode_flagged(const DevCodec &c, const DecodeArgs &a, const uint8_t *syn_ws,
+                                 hipStream_t s) {
+    if (a.ncw == 0) return hipSuccess;
+    const unsigned grid = (unsigned)((a.ncw + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_decode_flagged, dim3(grid), dim3(kBlock), 0, s, c, a, syn_ws);
+    return hipGetLastError();
+}
 
 hipError_t launch_encode_generic(const DevCodec &c, const EncodeArgs &a, hipStream_t s) {
     if (a.ncw == 0) return hipSuccess;

@@ -13,7 +13,7 @@ namespace ezrs {
 
 // Everything a kernel needs to know about a codec, passed by value at launch.
 struct DevCodec {
-    unsigned mm, nn, nroots, load, fcr, prim, iprim;
+    unsigned mm, nn, nroots, load, fcr, prim, iprim, poly;
     int dual;
     int masked;                   // symbol narrower than its datum (rs_base:1194)
     const uint16_t *alpha_to;     // device, nn+1
@@ -53,5 +53,15 @@ struct EncodeArgs {
 // Generic per-codeword kernels (ezrs_generic.hip): every codec, every length.
 hipError_t launch_encode_generic(const DevCodec &c, const EncodeArgs &a, hipStream_t s);
 hipError_t launch_decode_generic(const DevCodec &c, const DecodeArgs &a, hipStream_t s);
+// Error path behind the bit-sliced syndrome kernel: decodes the codewords whose result holds the
+// sentinel, starting from the syndromes in syn_ws ([ncw][32] bytes).
+hipError_t launch_decode_flagged(const DevCodec &c, const DecodeArgs &a, const uint8_t *syn_ws,
+                                 hipStream_t s);
+
+// Bit-sliced GF(2^8) kernels (ezrs_bitslice.hip) for the codecs of gen/ezrs_bs_tables.inc.
+int bitslice_codec_id(const DevCodec &d);   // -1 if the codec has no bit-sliced path
+hipError_t launch_bs_encode(int id, const EncodeArgs &a, hipStream_t s);
+hipError_t launch_bs_syndromes(int id, const DevCodec &d, const DecodeArgs &a, uint8_t *syn_ws,
+                               hipStream_t s);
 
 } // namespace ezrs

@@ -185,3 +185,55 @@ def test_c2_c3_full_size(torch):
     assert torch.equal(bad, cw)
     exp_pos = locs.sort(dim=1).values.to(torch.int32)       # PRIM = 1: ascending order
     assert torch.equal(pos[:, :12], exp_pos)
+
+
+@pytest.mark.parametrize("maker", ["RS(255,223)", "RS_CCSDS(255,223)", "RS_CCSDS_CONV(255,223)",
+                                   "RS(255,239)", "RS(255,251)"])
+@pytest.mark.parametrize("L,ncw,extra", [(1, 1, 0), (2, 511, 3), (63, 513, 0), (64, 777, 5),
+                                         (100, 1025, 1), (191, 600, 0)])
+def test_shapes_vs_oracle(torch, maker, L, ncw, extra):
+    """Shortened lengths (front padding of every width), batch sizes around the 512-codeword tile,
+    row strides wider than the codeword, and a separate parity buffer for encode."""
+    import ezrs
+    if maker.startswith("RS_CCSDS_CONV"):
+        c, params = ezrs.Codec.ccsds(223, dual=False), O.ccsds_params(223, False)
+    elif maker.startswith("RS_CCSDS"):
+        c, params = ezrs.Codec.ccsds(223), O.ccsds_params(223)
+    else:
+        k = int(maker[7:-1])
+        c, params = ezrs.Codec.rs(255, k), O.rs_params(255, k)
+    oc = O.Codec(*params)
+    nr = c.nroots
+    L = min(L, c.load)
+    rng = np.random.default_rng(L * 1000 + ncw)
+    stride = L + nr + extra
+    data = rng.integers(0, 256, (ncw, stride)).astype(np.uint8)
+    # encode into a separate parity buffer
+    par = np.zeros((ncw, nr), np.uint8)
+    exp_par = np.zeros((ncw, nr), np.uint8)
+    oc.encode_batch(data, L, exp_par, nthreads=8)
+    dd = torch.from_numpy(data).cuda()
+    dp = torch.from_numpy(par).cuda()
+    c.encode(dd, L, dp)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(dp.cpu().numpy(), exp_par)
+    # decode contiguous codewords (parity in-row), a few corrupted
+    cw = data.copy()
+    cw[:, L:L + nr] = exp_par
+    for k in range(0, ncw, 3):
+        m = int(rng.integers(1, nr // 2 + 2))
+        locs = rng.choice(L + nr, min(m, L + nr), replace=False)
+        cw[k, locs] ^= rng.integers(1, 256, len(locs)).astype(np.uint8)
+    exp = cw.copy()
+    exp_pos = np.zeros((ncw, nr), np.uint32)
+    exp_r = oc.decode_batch(exp, L, None, positions=exp_pos, nthreads=8)
+    dcw = torch.from_numpy(cw).cuda()
+    pos = torch.zeros((ncw, nr), dtype=torch.int32, device="cuda")
+    r = c.decode(dcw, L, None, positions=pos)
+    torch.cuda.synchronize()
+    r = r.cpu().numpy()
+    np.testing.assert_array_equal(r, exp_r)
+    np.testing.assert_array_equal(dcw.cpu().numpy(), exp)
+    pos = pos.cpu().numpy().view(np.uint32)
+    for k in np.nonzero(r > 0)[0]:
+        np.testing.assert_array_equal(pos[k, :r[k]], exp_pos[k, :r[k]])
