@@ -3,9 +3,9 @@
 
 The kernels evaluate syndromes S_i = r(g_i), g_i = alpha^((fcr+i)*prim) (c++/ezpwd/rs_base:1390-1414),
 on 32 slots per 32-bit register: 8 codewords x 4 interleaved segments (positions p = 4y + s).
-Per segment, Horner in d_i = g_i^4 runs in blocks of 16 y-steps:
+Per segment, Horner in d_i = g_i^4 runs in blocks of 8 y-steps (one 32-position LDS chunk):
 
-    G_i <- G_i * d_i^16 + sum_{t<16} c_{4(16k+t)+s} * d_i^(15-t)
+    G_i <- G_i * d_i^8 + sum_{t<8} c_{4(8k+t)+s} * d_i^(7-t)
 
 and the segments are folded with  S_i = g_i^2 (g_i G_0 + G_1) + (g_i G_2 + G_3).  Every constant
 multiplication is a GF(2)-linear 8x8 bit map; the tables below give, for every output bit, the
@@ -38,7 +38,7 @@ CODECS = [
 ]
 
 NROLES = 2
-BLOCK = 16     # y-steps per block (one LDS chunk = 64 positions)
+BLOCK = 8      # y-steps per block (one LDS chunk = 32 positions)
 
 
 def split(nr):
@@ -98,7 +98,7 @@ def gen_codec(name, poly, fcr, prim, nr, dual):
            f"    static constexpr int S0[2] = {{{roles[0][0]}, {roles[1][0]}}};",
            f"    static constexpr int NS[2] = {{{roles[0][1]}, {roles[1][1]}}};",
            "    template <int R> static __device__ void horner_chunk(uint32_t (&S)[16][8], "
-           "const uint32_t *tile, int lane, bool first);",
+           "const uint32_t *tile, int lb, bool first);",
            "    template <int R> static __device__ void fold(uint32_t (&S)[16][8]);",
            "    template <int R> static __device__ void parity_map(uint32_t (&S)[16][8], "
            "const uint32_t *qin, int lane);",
@@ -107,7 +107,7 @@ def gen_codec(name, poly, fcr, prim, nr, dual):
         I = "    "
         # ---- Horner chunk
         out.append(f"template <> __device__ __forceinline__ void {st}::horner_chunk<{r}>("
-                   "uint32_t (&S)[16][8], const uint32_t *tile, int lane, bool first) {")
+                   "uint32_t (&S)[16][8], const uint32_t *tile, int lb, bool first) {")
         out.append(f"{I}if (!first) {{")
         for i in range(n):
             rows = C.mul_rows(gf.pow(gf.pow(C.roots[r0 + i], 4), BLOCK))
@@ -123,7 +123,7 @@ def gen_codec(name, poly, fcr, prim, nr, dual):
             out.append(f"{I}{{ // y-step {t}")
             out.append(f"{I}    uint32_t P[8];")
             out.append(f"{I}    #pragma unroll")
-            out.append(f"{I}    for (int b = 0; b < 8; ++b) P[b] = tile[(lane + 64 * b) * 17 + {t}];")
+            out.append(f"{I}    for (int b = 0; b < 8; ++b) P[b] = tile[lb + 32 * b + {t}];")
             emit_combos(out, "l", ["P[0]", "P[1]", "P[2]", "P[3]"], I + "    ")
             emit_combos(out, "h", ["P[4]", "P[5]", "P[6]", "P[7]"], I + "    ")
             for i in range(n):

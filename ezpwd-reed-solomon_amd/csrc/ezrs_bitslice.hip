@@ -7,33 +7,47 @@
 // are formed once) and every output bit costs one v_bitop3_b32 (3-input XOR) per input byte.
 //
 // Work decomposition (one 128-thread workgroup = 2 waves = one 512-codeword tile):
-//   * lane l owns codewords tile0 + l + 64c, c = 0..7; its 32 register slots are (c, segment s),
-//     s = position mod 4, at bit 8s + c.  Segment interleaving keeps every step's input a natural
-//     little-endian dword of 4 consecutive symbols of one codeword (no byte shuffles).
+//   * lane l owns the 8 codewords at tile rows 32*(l>>2) + (l&3) + 4c, c = 0..7; its 32 register
+//     slots are (c, segment s), s = position mod 4, at bit 8s + c.  Segment interleaving keeps
+//     every step's input a natural little-endian dword of 4 consecutive symbols of one codeword.
 //   * wave r ("role") owns syndromes [S0[r], S0[r]+NS[r]): 16 syndromes x 8 bits = 128 state VGPRs.
-//   * the tile streams through LDS in chunks of 64 positions ([512 rows][17 dwords], odd row
-//     pitch: conflict-free column reads); each role bit-transposes half the chunk in place (3-stage
-//     delta swap, 48 ops per 8 dwords) so the transposition is not duplicated across the roles.
-//   * per chunk and role: state *= d^16, then 16 Horner y-steps (d = g^4) -- all constants are
-//     straight-line XOR networks generated from the codec (gen/ezrs_bs_tables.inc).
-//   * the 4 segment partials are folded in-register (tree: x g, << 8; x g^2, << 16), leaving the
+//   * the tile streams through LDS in chunks of 32 positions: 16 blocks of 32 rows x 32 bytes,
+//     block pitch 1028 B (one pad dword: a column read by 32 lanes hits 32 distinct banks).  Chunks
+//     arrive by LDS-DMA (global_load_lds_dwordx4, per-lane unaligned row addresses) into two
+//     buffers, so chunk k+1 streams in while chunk k is computed.
+//   * each role bit-transposes half of the chunk in place (3-stage delta swap, 48 ops per 8
+//     dwords); per chunk and role: state *= d^8, then 8 Horner y-steps (d = g^4) -- straight-line
+//     XOR networks generated from the codec (gen/ezrs_bs_tables.inc).
+//   * the 4 segment partials are folded in-register (x g, << 8; x g^2, << 16), leaving the
 //     syndromes of the lane's 8 codewords in byte lane 3.
 //
-// Decode (k_bs_syndromes): codewords whose 32 syndromes are zero (and carry no erasures) get
+// Decode (k_bs_syndromes): codewords whose syndromes are all zero (and carry no erasures) get
 // result 0 -- exactly what decode_symbols returns (rs_base:1416-1434); all others get a sentinel
-// and their syndromes are written to the workspace for the error-path kernel
-// (ezrs_generic.hip: decode_from_syndromes), which runs the reference's BM/Chien/Forney.
+// and their syndromes go to the workspace for the error-path kernel (ezrs_generic.hip:
+// k_decode_flagged), which runs the reference's BM/Chien/Forney on them.
 // Encode (k_bs_encode): syndromes of the data word -> parity via the GF(2) map Q (generated),
-// written straight to the caller's parity rows.
+// staged through LDS and stored as whole parity rows.
 #include "ezrs_internal.hpp"
 #include "gen/ezrs_bs_tables.inc"
 
 namespace ezrs {
 namespace bs {
 
-constexpr int kTile = 512;        // codewords per workgroup
-constexpr int kPitch = 17;        // LDS row pitch in dwords (64 data bytes + 4 pad)
+constexpr int kTile = 512;                 // codewords per workgroup
 constexpr int kThreads = 128;
+constexpr int kChunk = 32;                 // positions per LDS chunk
+constexpr int kBlockDw = 257;              // 32 rows x 8 dwords + 1 pad dword
+constexpr int kBufDw = 16 * kBlockDw;      // one chunk buffer (16 blocks)
+// Two chunk buffers; encode later reuses the space for the syndrome exchange (64 x 65 dwords) and
+// the parity image (512 rows x 32 bytes).
+constexpr int kLdsDw = 2 * kBufDw > 64 * 65 + kTile * 8 ? 2 * kBufDw : 64 * 65 + kTile * 8;
+constexpr int32_t kSentinel = INT32_MIN;
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+// LDS dword index of (lane, slot c, dword y of the chunk) is lane_base + 32 c + y.
+__device__ __forceinline__ int lane_base(int lane) { return (lane >> 2) * kBlockDw + (lane & 3) * 8; }
+__device__ __forceinline__ int tile_row(int lane, int c) { return 32 * (lane >> 2) + (lane & 3) + 4 * c; }
 
 // In-place 8x8 bit transpose of (register index) x (bit position mod 8): afterwards D[b] bit 8s+c
 // holds what D[c] bit 8s+b held.  3 delta-swap stages, 4 ops per register pair.
@@ -52,85 +66,107 @@ __device__ __forceinline__ void transpose8(uint32_t (&D)[8]) {
     }
 }
 
-// Stage chunk k (positions [64k, 64k+64) of the zero-front-padded word) of the tile into LDS.
-// Row rho = codeword cw0 + rho; symbol index u = position - pad; u < 0 reads as zero.
-__device__ __forceinline__ void load_chunk(uint32_t *tile, const uint8_t *base, size_t stride,
-                                           size_t cw0, size_t ncw, int k, int pad) {
-#pragma unroll 4
-    for (int j = 0; j < kTile * 4 / kThreads; ++j) {
-        const int pi = threadIdx.x + kThreads * j;
-        const int row = pi >> 2, q = pi & 3;
-        const size_t cw = cw0 + row;
-        const long u0 = 64L * k - pad + 16 * q;
-        uint32_t v[4] = {0u, 0u, 0u, 0u};
-        if (cw < ncw && u0 + 16 > 0) {
-            const uint8_t *p = base + cw * stride;
-            if ((long)(cw * stride) + u0 >= 0) {
-                __builtin_memcpy(v, p + u0, 16);
-            } else {
+struct Word {
+    const uint8_t *base;   // row 0 of the batch
+    size_t stride;         // bytes between rows
+    size_t cw0, ncw;       // first row of the tile, rows in the batch
+    int pad;               // leading zero positions (position = symbol index + pad)
+};
+
+// Issue this wave's 8 LDS-DMA pieces of chunk k: block b = 8*wave + i; lane j fetches row 32b + j/2,
+// bytes [32k - pad + 16 (j&1), +16) of it.  Rows past the batch re-read the last row (discarded);
+// pieces that would start before the batch are clamped (rebuilt by fixup_chunk0).
+__device__ __forceinline__ void issue_chunk(uint32_t *buf, const Word &w, int k) {
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+#pragma unroll 1
+    for (int i = 0; i < 8; ++i) {
+        const int b = 8 * wave + i;
+        size_t cw = w.cw0 + 32 * b + (lane >> 1);
+        if (cw >= w.ncw) cw = w.ncw - 1;
+        long off = (long)(cw * w.stride) + (long)kChunk * k - w.pad + 16 * (lane & 1);
+        if (off < 0) off = 0;
+        __builtin_amdgcn_global_load_lds(static_cast<const void *>(w.base + off),
+                                         (lds_void *)(buf + b * kBlockDw), 16, 0, 0);
+    }
+}
+
+// Chunk 0 holds the `pad` leading zero positions: zero them, and rebuild the rows whose DMA piece
+// was clamped at the start of the batch.
+__device__ __forceinline__ void fixup_chunk0(uint32_t *buf, const Word &w) {
+    for (int row = threadIdx.x; row < kTile; row += kThreads) {
+        uint32_t *r = buf + (row >> 5) * kBlockDw + (row & 31) * 8;
+        const size_t cw = w.cw0 + row;
+        if (cw < w.ncw && (long)(cw * w.stride) < w.pad) {
+            const uint8_t *p = w.base + cw * w.stride;
 #pragma unroll
-                for (int e = 0; e < 16; ++e)
-                    if (u0 + e >= 0) v[e >> 2] |= (uint32_t)p[u0 + e] << (8 * (e & 3));
-            }
-            if (u0 < 0) {
+            for (int d = 0; d < 8; ++d) {
+                uint32_t v = 0;
 #pragma unroll
-                for (int w = 0; w < 4; ++w) {
-                    const long lo = u0 + 4 * w;           // symbol index of byte 0 of dword w
-                    if (lo + 4 <= 0) v[w] = 0;
-                    else if (lo < 0) v[w] &= 0xFFFFFFFFu << (8 * (-lo));
+                for (int e = 0; e < 4; ++e) {
+                    const int u = 4 * d + e - w.pad;
+                    if (u >= 0) v |= (uint32_t)p[u] << (8 * e);
                 }
+                r[d] = v;
+            }
+        } else {
+#pragma unroll
+            for (int d = 0; d < 8; ++d) {
+                const int lo = 4 * d - w.pad;              // symbol index of byte 0 of dword d
+                if (lo + 4 <= 0) r[d] = 0;
+                else if (lo < 0) r[d] &= 0xFFFFFFFFu << (8 * (-lo));
             }
         }
-        uint32_t *d = tile + row * kPitch + 4 * q;
-        d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3];
     }
 }
 
-// In-place bit transposition of y-steps [8*role, 8*role+8) of the chunk: the dwords of the lane's
+// In-place bit transposition of y-steps [4*role, 4*role+4) of the chunk: the dwords of the lane's
 // 8 codewords become 8 bit-planes (plane b stored where codeword b's dword was).
-__device__ __forceinline__ void transpose_half(uint32_t *tile, int role, int lane) {
+__device__ __forceinline__ void transpose_half(uint32_t *buf, int role, int lb) {
 #pragma unroll 1
-    for (int yy = 0; yy < 8; ++yy) {
-        const int y = 8 * role + yy;
+    for (int yy = 0; yy < 4; ++yy) {
+        const int y = 4 * role + yy;
         uint32_t D[8];
 #pragma unroll
-        for (int c = 0; c < 8; ++c) D[c] = tile[(lane + 64 * c) * kPitch + y];
+        for (int c = 0; c < 8; ++c) D[c] = buf[lb + 32 * c + y];
         transpose8(D);
 #pragma unroll
-        for (int b = 0; b < 8; ++b) tile[(lane + 64 * b) * kPitch + y] = D[b];
+        for (int b = 0; b < 8; ++b) buf[lb + 32 * b + y] = D[b];
     }
 }
 
-// Run the Horner chunks of one word (decode: codeword, encode: data) through the tile.  Each role
-// runs its own copy of the loop (R is a template parameter): with a per-chunk role branch the
-// compiler hoists the common LDS plane loads of all 16 y-steps above the branch and spills.
+// Syndromes (in byte lane 3 after the fold) of the tile's words.  Each role runs its own copy of
+// the loop (R is a template parameter): with a per-chunk role branch the compiler hoists the
+// common LDS plane loads of all y-steps above the branch and spills.
 template <class C, int R>
-__device__ __forceinline__ void syndromes_tile(uint32_t (&S)[16][8], uint32_t *tile,
-                                               const uint8_t *base, size_t stride, size_t cw0,
-                                               size_t ncw, int nchunks, int pad) {
-    const int lane = threadIdx.x & 63;
+__device__ __forceinline__ void syndromes_tile(uint32_t (&S)[16][8], uint32_t *lds,
+                                               const Word &w, int nchunks) {
+    const int lb = lane_base(threadIdx.x & 63);
 #pragma unroll
     for (int i = 0; i < 16; ++i)
 #pragma unroll
         for (int q = 0; q < 8; ++q) S[i][q] = 0;
+    issue_chunk(lds, w, 0);
     for (int k = 0; k < nchunks; ++k) {
-        load_chunk(tile, base, stride, cw0, ncw, k, pad);
+        uint32_t *buf = lds + (k & 1) * kBufDw;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        transpose_half(tile, R, lane);
+        if (k == 0 && w.pad) {
+            fixup_chunk0(buf, w);
+            __syncthreads();
+        }
+        transpose_half(buf, R, lb);
         __syncthreads();
-        C::template horner_chunk<R>(S, tile, lane, k == 0);
-        __syncthreads();
+        if (k + 1 < nchunks) issue_chunk(lds + ((k + 1) & 1) * kBufDw, w, k + 1);
+        C::template horner_chunk<R>(S, buf, lb, k == 0);
     }
+    __syncthreads();
     C::template fold<R>(S);
 }
 
-// Byte lane 3 of 8 planes -> per-codeword bytes: after transpose8, R[c] >> 24 is the symbol of
-// codeword c.
+// Byte lane 3 of four registers -> one dword (register a in byte 0).
 __device__ __forceinline__ uint32_t pack4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
     return (a >> 24) | ((b >> 16) & 0xFF00u) | ((c >> 8) & 0xFF0000u) | (d & 0xFF000000u);
 }
-
-constexpr int32_t kSentinel = INT32_MIN;
 
 template <class C, int R>
 __device__ __forceinline__ uint32_t nonzero_mask(const uint32_t (&S)[16][8]) {
@@ -144,19 +180,19 @@ __device__ __forceinline__ uint32_t nonzero_mask(const uint32_t (&S)[16][8]) {
 
 // Write the role's syndromes of the flagged codewords (bits of fl) to their workspace slots.
 template <class C, int R>
-__device__ __forceinline__ void write_syndromes(uint32_t (&S)[16][8], uint32_t fl, size_t cw,
-                                                uint8_t *syn_ws) {
+__device__ __forceinline__ void write_syndromes(uint32_t (&S)[16][8], uint32_t fl, size_t cw0,
+                                                int lane, uint8_t *syn_ws) {
 #pragma unroll
     for (int i = 0; i < C::NS[R]; ++i) transpose8(S[i]);   // S[i][c] >> 24: codeword c's S_i
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
         if (!(fl >> c & 1)) continue;
-        uint8_t *dst = syn_ws + (cw + 64 * c) * 32 + C::S0[R];
+        uint8_t *dst = syn_ws + (cw0 + tile_row(lane, c)) * 32 + C::S0[R];
 #pragma unroll
         for (int i = 0; i < C::NS[R]; i += 4) {
             if (i + 4 <= C::NS[R]) {
-                const uint32_t w = pack4(S[i][c], S[i + 1][c], S[i + 2][c], S[i + 3][c]);
-                __builtin_memcpy(dst + i, &w, 4);
+                const uint32_t v = pack4(S[i][c], S[i + 1][c], S[i + 2][c], S[i + 3][c]);
+                __builtin_memcpy(dst + i, &v, 4);
             } else {
 #pragma unroll
                 for (int e = i; e < C::NS[R]; ++e) dst[e] = (uint8_t)(S[e][c] >> 24);
@@ -166,39 +202,36 @@ __device__ __forceinline__ void write_syndromes(uint32_t (&S)[16][8], uint32_t f
 }
 
 template <class C, int R>
-__device__ __forceinline__ void syndromes_body(uint32_t *tile, uint32_t (*flags)[64],
-                                               const uint8_t *data, size_t stride, unsigned nsym,
-                                               size_t ncw, const uint32_t *neras, int32_t *result,
+__device__ __forceinline__ void syndromes_body(uint32_t *lds, uint32_t (*flags)[64],
+                                               const Word &w, int nchunks,
+                                               const uint32_t *neras, int32_t *result,
                                                uint8_t *syn_ws) {
     const int lane = threadIdx.x & 63;
-    const size_t cw0 = (size_t)blockIdx.x * kTile;
-    const int nchunks = (int)((nsym + 63) / 64);
-    const int pad = nchunks * 64 - (int)nsym;
     uint32_t S[16][8];
-    syndromes_tile<C, R>(S, tile, data, stride, cw0, ncw, nchunks, pad);
+    syndromes_tile<C, R>(S, lds, w, nchunks);
     flags[R][lane] = nonzero_mask<C, R>(S);
     __syncthreads();
     uint32_t fl = flags[0][lane] | flags[1][lane];
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
-        const size_t cw = cw0 + lane + 64 * c;
-        if (cw >= ncw) { fl &= ~(1u << c); continue; }
+        const size_t cw = w.cw0 + tile_row(lane, c);
+        if (cw >= w.ncw) { fl &= ~(1u << c); continue; }
         if (neras && neras[cw]) fl |= 1u << c;      // erasures: the error path validates them
         if (R == 0) result[cw] = (fl >> c & 1) ? kSentinel : 0;
     }
-    if (fl) write_syndromes<C, R>(S, fl, cw0 + lane, syn_ws);
+    if (fl) write_syndromes<C, R>(S, fl, w.cw0, lane, syn_ws);
 }
 
 template <class C>
 __global__ void __launch_bounds__(kThreads, 2)
     k_bs_syndromes(const uint8_t *data, size_t stride, unsigned nsym, size_t ncw,
                    const uint32_t *neras, int32_t *result, uint8_t *syn_ws) {
-    __shared__ uint32_t tile[kTile * kPitch];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsDw];
     __shared__ uint32_t flags[2][64];
-    if (threadIdx.x < 64)
-        syndromes_body<C, 0>(tile, flags, data, stride, nsym, ncw, neras, result, syn_ws);
-    else
-        syndromes_body<C, 1>(tile, flags, data, stride, nsym, ncw, neras, result, syn_ws);
+    const int nchunks = (int)((nsym + kChunk - 1) / kChunk);
+    const Word w{data, stride, (size_t)blockIdx.x * kTile, ncw, nchunks * kChunk - (int)nsym};
+    if (threadIdx.x < 64) syndromes_body<C, 0>(lds, flags, w, nchunks, neras, result, syn_ws);
+    else syndromes_body<C, 1>(lds, flags, w, nchunks, neras, result, syn_ws);
 }
 
 template <class C, int R>
@@ -210,54 +243,72 @@ __device__ __forceinline__ void publish(const uint32_t (&S)[16][8], uint32_t *qi
     }
 }
 
+// Q map, then this role's parity bytes of the lane's 8 codewords into the LDS parity image
+// [512 rows][NR bytes, padded to a dword multiple].
 template <class C, int R>
-__device__ __forceinline__ void parity_store(uint32_t (&S)[16][8], const uint32_t *qin, int lane,
-                                             uint8_t *parity, size_t pstride, size_t cw,
-                                             size_t ncw) {
+__device__ __forceinline__ void parity_stage(uint32_t (&S)[16][8], const uint32_t *qin, int lane,
+                                             uint8_t *pimg, int ppitch) {
     C::template parity_map<R>(S, qin, lane);
 #pragma unroll
     for (int j = 0; j < C::NS[R]; ++j) transpose8(S[j]);  // S[j][c] >> 24: parity j of codeword c
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
-        if (cw + 64 * c >= ncw) continue;
-        uint8_t *dst = parity + (cw + 64 * c) * pstride + C::S0[R];
+        uint8_t *dst = pimg + tile_row(lane, c) * ppitch + C::S0[R];
 #pragma unroll
         for (int j = 0; j < C::NS[R]; j += 4) {
-            if (j + 4 <= C::NS[R]) {
-                const uint32_t w = pack4(S[j][c], S[j + 1][c], S[j + 2][c], S[j + 3][c]);
-                __builtin_memcpy(dst + j, &w, 4);
+            if (j + 4 <= C::NS[R] && ((C::S0[R] + j) & 3) == 0) {
+                *reinterpret_cast<uint32_t *>(dst + j) =
+                    pack4(S[j][c], S[j + 1][c], S[j + 2][c], S[j + 3][c]);
             } else {
 #pragma unroll
-                for (int e = j; e < C::NS[R]; ++e) dst[e] = (uint8_t)(S[e][c] >> 24);
+                for (int e = j; e < j + 4 && e < C::NS[R]; ++e) dst[e] = (uint8_t)(S[e][c] >> 24);
             }
         }
     }
 }
 
 template <class C, int R>
-__device__ __forceinline__ void encode_body(uint32_t *tile, const uint8_t *data, size_t stride,
-                                            unsigned len, uint8_t *parity, size_t pstride,
-                                            size_t ncw) {
+__device__ __forceinline__ void encode_body(uint32_t *lds, const Word &w, int nchunks,
+                                            uint8_t *parity, size_t pstride) {
     const int lane = threadIdx.x & 63;
-    const size_t cw0 = (size_t)blockIdx.x * kTile;
-    const int nchunks = (int)((len + 63) / 64);
-    const int pad = nchunks * 64 - (int)len;
     uint32_t S[16][8];
-    syndromes_tile<C, R>(S, tile, data, stride, cw0, ncw, nchunks, pad);
+    syndromes_tile<C, R>(S, lds, w, nchunks);
     // Both roles publish their syndromes (byte lane 3, 4 bit-planes per dword) for Q.
-    uint32_t *qin = tile;                           // [64 lanes][65 dwords]
+    uint32_t *qin = lds;                            // [64 lanes][65 dwords]
     publish<C, R>(S, qin, lane);
     __syncthreads();
-    parity_store<C, R>(S, qin, lane, parity, pstride, cw0 + lane, ncw);
+    constexpr int ppitch = (C::NR + 3) & ~3;
+    uint8_t *pimg = reinterpret_cast<uint8_t *>(lds + 64 * 65);
+    parity_stage<C, R>(S, qin, lane, pimg, ppitch);
+    __syncthreads();
+    // Whole parity rows out: 16-byte pieces, consecutive threads on consecutive pieces of a row.
+    constexpr int per_row = (C::NR + 15) / 16;
+    for (int pi = threadIdx.x; pi < kTile * per_row; pi += kThreads) {
+        const int row = pi / per_row, h = pi % per_row;
+        const size_t cw = w.cw0 + row;
+        if (cw >= w.ncw) continue;
+        const int n = C::NR - 16 * h < 16 ? C::NR - 16 * h : 16;
+        uint8_t *dst = parity + cw * pstride + 16 * h;
+        const uint8_t *src = pimg + row * ppitch + 16 * h;
+        if (n == 16) {
+            uint32_t v[4];
+            __builtin_memcpy(v, src, 16);
+            __builtin_memcpy(dst, v, 16);
+        } else {
+            for (int e = 0; e < n; ++e) dst[e] = src[e];
+        }
+    }
 }
 
 template <class C>
 __global__ void __launch_bounds__(kThreads, 2)
     k_bs_encode(const uint8_t *data, size_t stride, unsigned len, uint8_t *parity,
                 size_t pstride, size_t ncw) {
-    __shared__ uint32_t tile[kTile * kPitch];
-    if (threadIdx.x < 64) encode_body<C, 0>(tile, data, stride, len, parity, pstride, ncw);
-    else encode_body<C, 1>(tile, data, stride, len, parity, pstride, ncw);
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsDw];
+    const int nchunks = (int)((len + kChunk - 1) / kChunk);
+    const Word w{data, stride, (size_t)blockIdx.x * kTile, ncw, nchunks * kChunk - (int)len};
+    if (threadIdx.x < 64) encode_body<C, 0>(lds, w, nchunks, parity, pstride);
+    else encode_body<C, 1>(lds, w, nchunks, parity, pstride);
 }
 
 } // namespace bs
