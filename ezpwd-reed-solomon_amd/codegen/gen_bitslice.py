@@ -119,11 +119,21 @@ def gen_codec(name, poly, fcr, prim, nr, dual):
             out.append(f"{I}        __builtin_amdgcn_sched_barrier(0);")
             out.append(f"{I}    }}")
         out.append(f"{I}}}")
+        # raw dwords of y-step t+1 are loaded while y-step t computes; each y-step bit-transposes
+        # its 8 dwords (one per codeword slot) in registers
+        out.append(f"{I}uint32_t N[8];")
+        out.append(f"{I}#pragma unroll")
+        out.append(f"{I}for (int c = 0; c < 8; ++c) N[c] = tile[lb + 32 * c];")
         for t in range(BLOCK):
             out.append(f"{I}{{ // y-step {t}")
             out.append(f"{I}    uint32_t P[8];")
             out.append(f"{I}    #pragma unroll")
-            out.append(f"{I}    for (int b = 0; b < 8; ++b) P[b] = tile[lb + 32 * b + {t}];")
+            out.append(f"{I}    for (int c = 0; c < 8; ++c) P[c] = N[c];")
+            if t + 1 < BLOCK:
+                out.append(f"{I}    #pragma unroll")
+                out.append(f"{I}    for (int c = 0; c < 8; ++c) N[c] = tile[lb + 32 * c + {t + 1}];")
+            out.append(f"{I}    __builtin_amdgcn_sched_barrier(0);")
+            out.append(f"{I}    transpose8(P);")
             emit_combos(out, "l", ["P[0]", "P[1]", "P[2]", "P[3]"], I + "    ")
             emit_combos(out, "h", ["P[4]", "P[5]", "P[6]", "P[7]"], I + "    ")
             for i in range(n):
@@ -185,7 +195,23 @@ def main(dst=None):
             "// Straight-line XOR networks of the bit-sliced GF(2^8) RS kernels (see ezrs_bitslice.hip).",
             "#pragma once", "#include <cstdint>", "namespace ezrs { namespace bs {",
             "__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {",
-            "    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);", "}"]
+            "    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);", "}",
+            "// In-place 8x8 bit transpose of (register index) x (bit position mod 8): afterwards",
+            "// D[b] bit 8s+c holds what D[c] bit 8s+b held (3 delta-swap stages, 4 ops per pair).",
+            "__device__ __forceinline__ void transpose8(uint32_t (&D)[8]) {",
+            "#pragma unroll",
+            "    for (int k = 0; k < 3; ++k) {",
+            "        const int sh = 1 << k;",
+            "        const uint32_t M = k == 0 ? 0x55555555u : k == 1 ? 0x33333333u : 0x0F0F0F0Fu;",
+            "#pragma unroll",
+            "        for (int c = 0; c < 8; ++c) {",
+            "            if (c & sh) continue;",
+            "            const uint32_t x = D[c], y = D[c | sh];",
+            "            D[c] = (x & M) | ((y << sh) & ~M);",
+            "            D[c | sh] = ((x >> sh) & M) | (y & ~M);",
+            "        }",
+            "    }",
+            "}"]
     for c in CODECS:
         body.append(gen_codec(*c))
     body.append("#define EZRS_BS_CODEC_LIST(X) \\")

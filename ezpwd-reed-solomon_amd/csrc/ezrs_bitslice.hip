@@ -15,9 +15,10 @@
 //     block pitch 1028 B (one pad dword: a column read by 32 lanes hits 32 distinct banks).  Chunks
 //     arrive by LDS-DMA (global_load_lds_dwordx4, per-lane unaligned row addresses) into two
 //     buffers, so chunk k+1 streams in while chunk k is computed.
-//   * each role bit-transposes half of the chunk in place (3-stage delta swap, 48 ops per 8
-//     dwords); per chunk and role: state *= d^8, then 8 Horner y-steps (d = g^4) -- straight-line
-//     XOR networks generated from the codec (gen/ezrs_bs_tables.inc).
+//   * per chunk and role: state *= d^8, then 8 Horner y-steps (d = g^4); each y-step reads the 8
+//     raw dwords of its slots from LDS (the next step's are in flight meanwhile) and bit-transposes
+//     them in registers (3-stage delta swap, 48 ops) -- straight-line XOR networks generated from
+//     the codec (gen/ezrs_bs_tables.inc).
 //   * the 4 segment partials are folded in-register (x g, << 8; x g^2, << 16), leaving the
 //     syndromes of the lane's 8 codewords in byte lane 3.
 //
@@ -48,23 +49,6 @@ typedef __attribute__((address_space(3))) void lds_void;
 // LDS dword index of (lane, slot c, dword y of the chunk) is lane_base + 32 c + y.
 __device__ __forceinline__ int lane_base(int lane) { return (lane >> 2) * kBlockDw + (lane & 3) * 8; }
 __device__ __forceinline__ int tile_row(int lane, int c) { return 32 * (lane >> 2) + (lane & 3) + 4 * c; }
-
-// In-place 8x8 bit transpose of (register index) x (bit position mod 8): afterwards D[b] bit 8s+c
-// holds what D[c] bit 8s+b held.  3 delta-swap stages, 4 ops per register pair.
-__device__ __forceinline__ void transpose8(uint32_t (&D)[8]) {
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const int sh = 1 << k;
-        const uint32_t M = k == 0 ? 0x55555555u : k == 1 ? 0x33333333u : 0x0F0F0F0Fu;
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            if (c & sh) continue;
-            const uint32_t x = D[c], y = D[c | sh];
-            D[c] = (x & M) | ((y << sh) & ~M);
-            D[c | sh] = ((x >> sh) & M) | (y & ~M);
-        }
-    }
-}
 
 struct Word {
     const uint8_t *base;   // row 0 of the batch
@@ -119,21 +103,6 @@ __device__ __forceinline__ void fixup_chunk0(uint32_t *buf, const Word &w) {
     }
 }
 
-// In-place bit transposition of y-steps [4*role, 4*role+4) of the chunk: the dwords of the lane's
-// 8 codewords become 8 bit-planes (plane b stored where codeword b's dword was).
-__device__ __forceinline__ void transpose_half(uint32_t *buf, int role, int lb) {
-#pragma unroll 1
-    for (int yy = 0; yy < 4; ++yy) {
-        const int y = 4 * role + yy;
-        uint32_t D[8];
-#pragma unroll
-        for (int c = 0; c < 8; ++c) D[c] = buf[lb + 32 * c + y];
-        transpose8(D);
-#pragma unroll
-        for (int b = 0; b < 8; ++b) buf[lb + 32 * b + y] = D[b];
-    }
-}
-
 // Syndromes (in byte lane 3 after the fold) of the tile's words.  Each role runs its own copy of
 // the loop (R is a template parameter): with a per-chunk role branch the compiler hoists the
 // common LDS plane loads of all y-steps above the branch and spills.
@@ -145,7 +114,9 @@ __device__ __forceinline__ void syndromes_tile(uint32_t (&S)[16][8], uint32_t *l
     for (int i = 0; i < 16; ++i)
 #pragma unroll
         for (int q = 0; q < 8; ++q) S[i][q] = 0;
+#ifndef EZRS_BS_ABLATE_DMA
     issue_chunk(lds, w, 0);
+#endif
     for (int k = 0; k < nchunks; ++k) {
         uint32_t *buf = lds + (k & 1) * kBufDw;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -154,10 +125,14 @@ __device__ __forceinline__ void syndromes_tile(uint32_t (&S)[16][8], uint32_t *l
             fixup_chunk0(buf, w);
             __syncthreads();
         }
-        transpose_half(buf, R, lb);
-        __syncthreads();
+#ifndef EZRS_BS_ABLATE_DMA   // timing-only builds (tools/micro/bs_ablate): drop the HBM stream
         if (k + 1 < nchunks) issue_chunk(lds + ((k + 1) & 1) * kBufDw, w, k + 1);
+#endif
+#ifndef EZRS_BS_ABLATE_COMPUTE  // timing-only builds: drop the XOR networks
         C::template horner_chunk<R>(S, buf, lb, k == 0);
+#else
+        S[0][0] ^= buf[lb];
+#endif
     }
     __syncthreads();
     C::template fold<R>(S);
