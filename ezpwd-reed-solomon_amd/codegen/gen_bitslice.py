@@ -3,9 +3,9 @@
 
 The kernels evaluate syndromes S_i = r(g_i), g_i = alpha^((fcr+i)*prim) (c++/ezpwd/rs_base:1390-1414),
 on 32 slots per 32-bit register: 8 codewords x 4 interleaved segments (positions p = 4y + s).
-Per segment, Horner in d_i = g_i^4 runs in blocks of 8 y-steps (one 32-position LDS chunk):
+Per segment, Horner in d_i = g_i^4 runs in blocks of 16 y-steps (64 positions):
 
-    G_i <- G_i * d_i^8 + sum_{t<8} c_{4(8k+t)+s} * d_i^(7-t)
+    G_i <- G_i * d_i^16 + sum_{t<16} c_{4(16k+t)+s} * d_i^(15-t)
 
 and the segments are folded with  S_i = g_i^2 (g_i G_0 + G_1) + (g_i G_2 + G_3).  Every constant
 multiplication is a GF(2)-linear 8x8 bit map; the tables below give, for every output bit, the
@@ -13,8 +13,8 @@ multiplication is a GF(2)-linear 8x8 bit map; the tables below give, for every o
 each input nibble once and spend one v_bitop3 per output bit and input byte).
 
 Encode evaluates the data word only and maps the syndromes to parity with the GF(2) matrix Q of
-parity = into_dual?( V^-1 (g^NR * H(data)) ) (see gf8.Codec8.q_rows); its table QN gives, per
-output bit and input syndrome, the (lo, hi) nibble masks.
+parity = into_dual?( V^-1 (g^NR * H(data)) ) (see gf8.Codec8.q_rows), in passes of 8 parity
+symbols over full 32-codeword registers (q_pass).
 
 Dual-basis codecs fold from_dual into every input map and into_dual into Q, so the kernels never
 touch the dual-basis tables (rs_base:109-146, 1312, 1324-1326).
@@ -37,13 +37,18 @@ CODECS = [
     ("CCSDS_CONV_255_223", 0x187, 112, 11, 32, False),
 ]
 
-NROLES = 2
-BLOCK = 8      # y-steps per block (one LDS chunk = 32 positions)
+NROLES = 4
+BLOCK = 16     # y-steps per Horner block (an LDS chunk of 128 positions = 2 blocks)
 
 
 def split(nr):
-    h = (nr + 1) // 2
-    return [(0, h), (h, nr - h)]
+    """Syndromes per role: NROLES contiguous ranges (first, count)."""
+    h = (nr + NROLES - 1) // NROLES
+    out = []
+    for r in range(NROLES):
+        a = min(nr, r * h)
+        out.append((a, min(nr, a + h) - a))
+    return out
 
 
 def nib(row):
@@ -91,61 +96,67 @@ def gen_codec(name, poly, fcr, prim, nr, dual):
     gf = C.gf
     roles = split(nr)
     Q = C.q_rows()
+    npass = (nr + 7) // 8
     st = f"BS_{name}"
     out = [f"struct {st} {{",
            f"    static constexpr unsigned POLY = {poly:#x}, FCR = {fcr}, PRIM = {prim}, NR = {nr};",
            f"    static constexpr bool DUAL = {'true' if dual else 'false'};",
-           f"    static constexpr int S0[2] = {{{roles[0][0]}, {roles[1][0]}}};",
-           f"    static constexpr int NS[2] = {{{roles[0][1]}, {roles[1][1]}}};",
-           "    template <int R> static __device__ void horner_chunk(uint32_t (&S)[16][8], "
-           "const uint32_t *tile, int lb, bool first);",
+           f"    static constexpr int NROLES = {NROLES};",
+           f"    static constexpr int S0[{NROLES}] = {{{', '.join(str(a) for a, _ in roles)}}};",
+           f"    static constexpr int NS[{NROLES}] = {{{', '.join(str(n) for _, n in roles)}}};",
+           f"    static constexpr int NPASS = {npass};   // parity passes of 8 symbols",
+           "    template <int R> static __device__ void block_mul(uint32_t (&S)[16][8]);",
+           "    template <int R, int H> static __device__ void horner_half(uint32_t (&S)[16][8], "
+           "const uint32_t *p);",
            "    template <int R> static __device__ void fold(uint32_t (&S)[16][8]);",
-           "    template <int R> static __device__ void parity_map(uint32_t (&S)[16][8], "
-           "const uint32_t *qin, int lane);",
+           "    template <int P> static __device__ void q_pass(uint32_t (&O)[8][8], "
+           "const uint32_t *in, int ld);",
            "};"]
+    H = BLOCK // 2
     for r, (r0, n) in enumerate(roles):
         I = "    "
-        # ---- Horner chunk
-        out.append(f"template <> __device__ __forceinline__ void {st}::horner_chunk<{r}>("
-                   "uint32_t (&S)[16][8], const uint32_t *tile, int lb, bool first) {")
-        out.append(f"{I}if (!first) {{")
+        # ---- state *= d^BLOCK
+        out.append(f"template <> __device__ __forceinline__ void {st}::block_mul<{r}>(uint32_t (&S)[16][8]) {{")
         for i in range(n):
             rows = C.mul_rows(gf.pow(gf.pow(C.roots[r0 + i], 4), BLOCK))
-            out.append(f"{I}    {{")
-            emit_combos(out, "l", [f"S[{i}][{q}]" for q in range(4)], I + "        ")
-            emit_combos(out, "h", [f"S[{i}][{q}]" for q in range(4, 8)], I + "        ")
+            out.append(f"{I}{{")
+            emit_combos(out, "l", [f"S[{i}][{q}]" for q in range(4)], I + "    ")
+            emit_combos(out, "h", [f"S[{i}][{q}]" for q in range(4, 8)], I + "    ")
             for q in range(8):
-                out.append(f"{I}        " + upd(f"S[{i}][{q}]", None, nib(rows[q])))
-            out.append(f"{I}        __builtin_amdgcn_sched_barrier(0);")
-            out.append(f"{I}    }}")
-        out.append(f"{I}}}")
-        # raw dwords of y-step t+1 are loaded while y-step t computes; each y-step bit-transposes
-        # its 8 dwords (one per codeword slot) in registers
-        out.append(f"{I}uint32_t N[8];")
-        out.append(f"{I}#pragma unroll")
-        out.append(f"{I}for (int c = 0; c < 8; ++c) N[c] = tile[lb + 32 * c];")
-        for t in range(BLOCK):
-            out.append(f"{I}{{ // y-step {t}")
-            out.append(f"{I}    uint32_t P[8];")
-            out.append(f"{I}    #pragma unroll")
-            out.append(f"{I}    for (int c = 0; c < 8; ++c) P[c] = N[c];")
-            if t + 1 < BLOCK:
-                out.append(f"{I}    #pragma unroll")
-                out.append(f"{I}    for (int c = 0; c < 8; ++c) N[c] = tile[lb + 32 * c + {t + 1}];")
-            out.append(f"{I}    __builtin_amdgcn_sched_barrier(0);")
-            out.append(f"{I}    transpose8(P);")
-            emit_combos(out, "l", ["P[0]", "P[1]", "P[2]", "P[3]"], I + "    ")
-            emit_combos(out, "h", ["P[4]", "P[5]", "P[6]", "P[7]"], I + "    ")
-            for i in range(n):
-                d = gf.pow(C.roots[r0 + i], 4)
-                rows = C.input_rows(gf.pow(d, BLOCK - 1 - t))
-                for q in range(8):
-                    ln = upd(f"S[{i}][{q}]", f"S[{i}][{q}]", nib(rows[q]))
-                    if ln:
-                        out.append(f"{I}    " + ln)
+                out.append(f"{I}    " + upd(f"S[{i}][{q}]", None, nib(rows[q])))
             out.append(f"{I}    __builtin_amdgcn_sched_barrier(0);")
             out.append(f"{I}}}")
         out.append("}")
+        # ---- half blocks: y-steps [H*half, H*half + H) of a block, constants d^(BLOCK-1-t)
+        for half in range(2):
+            out.append(f"template <> __device__ __forceinline__ void {st}::horner_half<{r}, {half}>("
+                       "uint32_t (&S)[16][8], const uint32_t *p) {")
+            # bit-planes of y-step t (8 dwords at p[32 b + t]) arrive while y-step t-1 computes
+            out.append(f"{I}uint32_t N[8];")
+            out.append(f"{I}#pragma unroll")
+            out.append(f"{I}for (int b = 0; b < 8; ++b) N[b] = p[32 * b];")
+            for tt in range(H):
+                t = half * H + tt
+                out.append(f"{I}{{ // y-step {t}")
+                out.append(f"{I}    uint32_t P[8];")
+                out.append(f"{I}    #pragma unroll")
+                out.append(f"{I}    for (int b = 0; b < 8; ++b) P[b] = N[b];")
+                if tt + 1 < H:
+                    out.append(f"{I}    #pragma unroll")
+                    out.append(f"{I}    for (int b = 0; b < 8; ++b) N[b] = p[32 * b + {tt + 1}];")
+                out.append(f"{I}    __builtin_amdgcn_sched_barrier(0);")
+                emit_combos(out, "l", ["P[0]", "P[1]", "P[2]", "P[3]"], I + "    ")
+                emit_combos(out, "h", ["P[4]", "P[5]", "P[6]", "P[7]"], I + "    ")
+                for i in range(n):
+                    d = gf.pow(C.roots[r0 + i], 4)
+                    rows = C.input_rows(gf.pow(d, BLOCK - 1 - t))
+                    for q in range(8):
+                        ln = upd(f"S[{i}][{q}]", f"S[{i}][{q}]", nib(rows[q]))
+                        if ln:
+                            out.append(f"{I}    " + ln)
+                out.append(f"{I}    __builtin_amdgcn_sched_barrier(0);")
+                out.append(f"{I}}}")
+            out.append("}")
         # ---- segment fold
         out.append(f"template <> __device__ __forceinline__ void {st}::fold<{r}>(uint32_t (&S)[16][8]) {{")
         for lvl, sh in ((1, 8), (2, 16)):
@@ -162,24 +173,37 @@ def gen_codec(name, poly, fcr, prim, nr, dual):
                 out.append(f"{I}    __builtin_amdgcn_sched_barrier(0);")
                 out.append(f"{I}}}")
         out.append("}")
-        # ---- encode parity map
-        out.append(f"template <> __device__ __forceinline__ void {st}::parity_map<{r}>("
-                   "uint32_t (&S)[16][8], const uint32_t *qin, int lane) {")
-        first = [[True] * 8 for _ in range(n)]
+    # ---- encode parity map, one pass of up to 8 parity symbols over full 32-slot registers:
+    # O[jl][b] = bit b of parity symbol 8P+jl; in[(8 i + q) * ld] = bit q of syndrome i.
+    for P in range(npass):
+        I = "    "
+        j0, nj = 8 * P, min(8, nr - 8 * P)
+        out.append(f"template <> __device__ __forceinline__ void {st}::q_pass<{P}>("
+                   "uint32_t (&O)[8][8], const uint32_t *in, int ld) {")
+        first = [[True] * 8 for _ in range(nj)]
+        out.append(f"{I}uint32_t N[8];")
+        out.append(f"{I}#pragma unroll")
+        out.append(f"{I}for (int q = 0; q < 8; ++q) N[q] = in[q * ld];")
         for i in range(nr):
             out.append(f"{I}{{ // syndrome {i}")
-            out.append(f"{I}    const uint32_t w0 = qin[lane * 65 + {2 * i}], w1 = qin[lane * 65 + {2 * i + 1}];")
-            emit_combos(out, "l", ["(w0 << 24)", "(w0 << 16)", "(w0 << 8)", "w0"], I + "    ")
-            emit_combos(out, "h", ["(w1 << 24)", "(w1 << 16)", "(w1 << 8)", "w1"], I + "    ")
-            for jl in range(n):
+            out.append(f"{I}    uint32_t P[8];")
+            out.append(f"{I}    #pragma unroll")
+            out.append(f"{I}    for (int q = 0; q < 8; ++q) P[q] = N[q];")
+            if i + 1 < nr:
+                out.append(f"{I}    #pragma unroll")
+                out.append(f"{I}    for (int q = 0; q < 8; ++q) N[q] = in[({8 * (i + 1)} + q) * ld];")
+            out.append(f"{I}    __builtin_amdgcn_sched_barrier(0);")
+            emit_combos(out, "l", ["P[0]", "P[1]", "P[2]", "P[3]"], I + "    ")
+            emit_combos(out, "h", ["P[4]", "P[5]", "P[6]", "P[7]"], I + "    ")
+            for jl in range(nj):
                 for b in range(8):
-                    row = Q[8 * (r0 + jl) + b]
+                    row = Q[8 * (j0 + jl) + b]
                     m = nib((row >> (8 * i)) & 0xFF)
                     if first[jl][b]:
-                        out.append(f"{I}    " + upd(f"S[{jl}][{b}]", None, m))
+                        out.append(f"{I}    " + upd(f"O[{jl}][{b}]", None, m))
                         first[jl][b] = False
                     else:
-                        ln = upd(f"S[{jl}][{b}]", f"S[{jl}][{b}]", m)
+                        ln = upd(f"O[{jl}][{b}]", f"O[{jl}][{b}]", m)
                         if ln:
                             out.append(f"{I}    " + ln)
             out.append(f"{I}    __builtin_amdgcn_sched_barrier(0);")

@@ -201,9 +201,35 @@ int reserve_syn(ezrs_codec *c, size_t ncw) {
         c->d_syn = nullptr;
         c->syn_cap = 0;
     }
-    HIP_TRY(hipMalloc(&c->d_syn, ncw * 32));
+    HIP_TRY(hipMalloc(&c->d_syn, bs_encode_ws_bytes(ncw)));   // >= ncw * 32 (decode's need)
     c->syn_cap = ncw;
     return 0;
+}
+
+} // namespace
+
+namespace {
+
+// The one place that picks kernels: every entry point (device or host-memory) goes through these.
+// ws: bs_encode_ws_bytes(ncw) bytes (bit-sliced path only).
+hipError_t dispatch_encode(const ezrs_codec *c, const EncodeArgs &a, void *ws, hipStream_t st) {
+    return c->bs_id >= 0 ? launch_bs_encode(c->bs_id, a, ws, st) : launch_encode_generic(c->dev, a, st);
+}
+
+// syn_ws: [ncw][32] bytes (bit-sliced path only).
+hipError_t dispatch_decode(const ezrs_codec *c, const DecodeArgs &a, uint8_t *syn_ws,
+                           hipStream_t st) {
+    const unsigned w = c->dev.mm <= 8 ? 1 : 2;
+    const bool contiguous = a.parity == static_cast<char *>(a.data) + (size_t)a.len * w &&
+                            a.parity_stride == a.data_stride;
+    if (c->bs_id >= 0 && contiguous) {
+        // Bit-sliced syndromes for the whole batch; the reference algorithm only for the codewords
+        // that are not valid as received (or carry erasures to validate).
+        hipError_t e = launch_bs_syndromes(c->bs_id, c->dev, a, syn_ws, st);
+        if (e == hipSuccess) e = launch_decode_flagged(c->dev, a, syn_ws, st);
+        return e;
+    }
+    return launch_decode_generic(c->dev, a, st);
 }
 
 } // namespace
@@ -230,8 +256,8 @@ int ezrs_encode(const ezrs_codec *c, const void *data, size_t data_stride, unsig
     if (ncw > 1 && data_stride < len) return -EINVAL;
     DeviceGuard g(c->device);
     EncodeArgs a{data, data_stride, len, parity, parity_stride, ncw};
-    hipError_t e = c->bs_id >= 0 ? launch_bs_encode(c->bs_id, a, static_cast<hipStream_t>(stream))
-                                 : launch_encode_generic(c->dev, a, static_cast<hipStream_t>(stream));
+    if (int r = reserve_syn(const_cast<ezrs_codec *>(c), ncw)) return r;
+    hipError_t e = dispatch_encode(c, a, c->d_syn, static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return hip_fail(e, "encode launch");
     return 0;
 }
@@ -260,19 +286,8 @@ int ezrs_decode(const ezrs_codec *c, void *data, size_t data_stride, unsigned le
     DeviceGuard g(c->device);
     DecodeArgs a{data, data_stride, len, parity, parity_stride, eras, eras_stride, neras,
                  result, positions, pos_stride, corr, corr_stride, ncw};
-    hipStream_t st = static_cast<hipStream_t>(stream);
-    const bool contiguous =
-        parity == static_cast<char *>(data) + (size_t)len * w && parity_stride == data_stride;
-    hipError_t e;
-    if (c->bs_id >= 0 && contiguous) {
-        // Bit-sliced syndromes for the whole batch; the reference algorithm only for the codewords
-        // that are not valid as received (or carry erasures to validate).
-        if (int r = reserve_syn(const_cast<ezrs_codec *>(c), ncw)) return r;
-        e = launch_bs_syndromes(c->bs_id, c->dev, a, c->d_syn, st);
-        if (e == hipSuccess) e = launch_decode_flagged(c->dev, a, c->d_syn, st);
-    } else {
-        e = launch_decode_generic(c->dev, a, st);
-    }
+    if (int r = reserve_syn(const_cast<ezrs_codec *>(c), ncw)) return r;
+    hipError_t e = dispatch_decode(c, a, c->d_syn, static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return hip_fail(e, "decode launch");
     return 0;
 }
@@ -321,8 +336,9 @@ int ezrs_encode_host(ezrs_codec *c, const void *data, size_t data_stride, unsign
     DeviceGuard g(c->device);
     if (!chunk) chunk = default_chunk((size_t)(len + NR) * w);
     if (chunk > ncw) chunk = ncw;
-    const size_t dbytes = align_up(chunk * len * w), pbytes = align_up(chunk * NR * w);
-    if (int r = ensure_stage(c, dbytes + pbytes)) return r;
+    const size_t dbytes = align_up(chunk * len * w), pbytes = align_up(chunk * NR * w),
+                 wbytes = c->bs_id >= 0 ? align_up(bs_encode_ws_bytes(chunk)) : 0;
+    if (int r = ensure_stage(c, dbytes + pbytes + wbytes)) return r;
     for (size_t i = 0, k0 = 0; k0 < ncw; ++i, k0 += chunk) {
         const int s = (int)(i & 1);
         hipStream_t st = c->streams[s];
@@ -333,7 +349,7 @@ int ezrs_encode_host(ezrs_codec *c, const void *data, size_t data_stride, unsign
                                  static_cast<const char *>(data) + k0 * data_stride * w,
                                  data_stride * w, (size_t)len * w, n, hipMemcpyHostToDevice, st));
         EncodeArgs a{dd, len, len, dp, NR, n};
-        HIP_TRY(launch_encode_generic(c->dev, a, st));
+        HIP_TRY(dispatch_encode(c, a, dp + pbytes, st));
         HIP_TRY(hipMemcpy2DAsync(static_cast<char *>(parity) + k0 * parity_stride * w,
                                  parity_stride * w, dp, (size_t)NR * w, (size_t)NR * w, n,
                                  hipMemcpyDeviceToHost, st));
@@ -345,7 +361,7 @@ int ezrs_encode_host(ezrs_codec *c, const void *data, size_t data_stride, unsign
 int ezrs_decode_host(ezrs_codec *c, void *data, size_t data_stride, unsigned len, void *parity,
                      size_t parity_stride, const uint32_t *eras, size_t eras_stride,
                      const uint32_t *neras, int32_t *result, uint32_t *positions,
-                     size_t pos_stride, size_t ncw, size_t chunk) {
+                     size_t pos_stride, void *corr, size_t corr_stride, size_t ncw, size_t chunk) {
     if (!c) return -EINVAL;
     if (ncw == 0) return 0;
     if (!data || !result) return -EINVAL;
@@ -358,6 +374,7 @@ int ezrs_decode_host(ezrs_codec *c, void *data, size_t data_stride, unsigned len
     if (ncw > 1 && (data_stride < len || parity_stride < NR)) return -EINVAL;
     if (neras && !eras) return -EINVAL;
     if (positions && ncw > 1 && pos_stride < NR) return -EINVAL;
+    if (corr && ncw > 1 && corr_stride < NR) return -EINVAL;
     const size_t ecols = eras ? (eras_stride < NR ? eras_stride : NR) : 0;
     if (eras && ecols == 0 && ncw > 1) return -EINVAL;
     std::lock_guard<std::mutex> lk(c->mu);
@@ -367,15 +384,18 @@ int ezrs_decode_host(ezrs_codec *c, void *data, size_t data_stride, unsigned len
     if (chunk > ncw) chunk = ncw;
     const size_t b_cw = align_up(chunk * row), b_er = align_up(chunk * ecols * 4),
                  b_ne = align_up(neras ? chunk * 4 : 0), b_rs = align_up(chunk * 4),
-                 b_ps = align_up(positions ? chunk * NR * 4 : 0);
-    if (int r = ensure_stage(c, b_cw + b_er + b_ne + b_rs + b_ps)) return r;
+                 b_ps = align_up(positions ? chunk * NR * 4 : 0),
+                 b_co = align_up(corr ? chunk * NR * w : 0),
+                 b_sy = align_up(c->bs_id >= 0 ? chunk * 32 : 0);
+    if (int r = ensure_stage(c, b_cw + b_er + b_ne + b_rs + b_ps + b_co + b_sy)) return r;
     for (size_t i = 0, k0 = 0; k0 < ncw; ++i, k0 += chunk) {
         const int s = (int)(i & 1);
         hipStream_t st = c->streams[s];
         const size_t n = ncw - k0 < chunk ? ncw - k0 : chunk;
         if (i >= 2) HIP_TRY(hipStreamSynchronize(st));
         char *base = static_cast<char *>(c->d_stage[s]);
-        char *dcw = base, *der = dcw + b_cw, *dne = der + b_er, *drs = dne + b_ne, *dps = drs + b_rs;
+        char *dcw = base, *der = dcw + b_cw, *dne = der + b_er, *drs = dne + b_ne, *dps = drs + b_rs,
+             *dco = dps + b_ps, *dsy = dco + b_co;
         char *hd = static_cast<char *>(data) + k0 * data_stride * w;
         char *hp = static_cast<char *>(parity) + k0 * parity_stride * w;
         HIP_TRY(hipMemcpy2DAsync(dcw, row, hd, data_stride * w, (size_t)len * w, n,
@@ -389,12 +409,16 @@ int ezrs_decode_host(ezrs_codec *c, void *data, size_t data_stride, unsigned len
         if (positions)
             HIP_TRY(hipMemcpy2DAsync(dps, (size_t)NR * 4, positions + k0 * pos_stride,
                                      pos_stride * 4, (size_t)NR * 4, n, hipMemcpyHostToDevice, st));
+        if (corr)   // corr is copy-in/copy-out: entries the decode does not write keep their value
+            HIP_TRY(hipMemcpy2DAsync(dco, (size_t)NR * w, static_cast<char *>(corr) + k0 * corr_stride * w,
+                                     corr_stride * w, (size_t)NR * w, n, hipMemcpyHostToDevice, st));
         DecodeArgs a{dcw, len + NR, len, dcw + (size_t)len * w, len + NR,
                      eras ? reinterpret_cast<uint32_t *>(der) : nullptr, ecols,
                      neras ? reinterpret_cast<uint32_t *>(dne) : nullptr,
                      reinterpret_cast<int32_t *>(drs),
-                     positions ? reinterpret_cast<uint32_t *>(dps) : nullptr, NR, nullptr, 0, n};
-        HIP_TRY(launch_decode_generic(c->dev, a, st));
+                     positions ? reinterpret_cast<uint32_t *>(dps) : nullptr, NR,
+                     corr ? dco : nullptr, NR, n};
+        HIP_TRY(dispatch_decode(c, a, reinterpret_cast<uint8_t *>(dsy), st));
         HIP_TRY(hipMemcpy2DAsync(hd, data_stride * w, dcw, row, (size_t)len * w, n,
                                  hipMemcpyDeviceToHost, st));
         HIP_TRY(hipMemcpy2DAsync(hp, parity_stride * w, dcw + (size_t)len * w, row,
@@ -403,6 +427,9 @@ int ezrs_decode_host(ezrs_codec *c, void *data, size_t data_stride, unsigned len
         if (positions)
             HIP_TRY(hipMemcpy2DAsync(positions + k0 * pos_stride, pos_stride * 4, dps,
                                      (size_t)NR * 4, (size_t)NR * 4, n, hipMemcpyDeviceToHost, st));
+        if (corr)
+            HIP_TRY(hipMemcpy2DAsync(static_cast<char *>(corr) + k0 * corr_stride * w, corr_stride * w,
+                                     dco, (size_t)NR * w, (size_t)NR * w, n, hipMemcpyDeviceToHost, st));
     }
     for (int s = 0; s < 2; ++s) HIP_TRY(hipStreamSynchronize(c->streams[s]));
     return 0;

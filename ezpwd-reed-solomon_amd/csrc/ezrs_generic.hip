@@ -300,11 +300,13 @@ constexpr int32_t kSentinel = INT32_MIN;
 __global__ void __launch_bounds__(kBlock) k_decode_flagged(DevCodec c, DecodeArgs a,
                                                            const uint8_t *syn_ws) {
     __shared__ __attribute__((aligned(16))) uint16_t smem[2 * 256 + 256];
+    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool mine = k < a.ncw && a.result[k] == kSentinel;
+    if (!__syncthreads_or(mine)) return;     // the common case: a clean block leaves at once
     const uint16_t *A, *I;
     const uint8_t *ID, *FD;
     stage_tables<true>(c, smem, A, I, ID, FD);
-    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= a.ncw || a.result[k] != kSentinel) return;
+    if (!mine) return;
     uint8_t *data = static_cast<uint8_t *>(a.data) + k * a.data_stride;
     uint8_t *parity = static_cast<uint8_t *>(a.parity) + k * a.parity_stride;
     const uint32_t *eras = a.eras ? a.eras + k * a.eras_stride : nullptr;

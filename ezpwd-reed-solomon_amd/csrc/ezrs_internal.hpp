@@ -60,7 +60,9 @@ hipError_t launch_decode_flagged(const DevCodec &c, const DecodeArgs &a, const u
 
 // Bit-sliced GF(2^8) kernels (ezrs_bitslice.hip) for the codecs of gen/ezrs_bs_tables.inc.
 int bitslice_codec_id(const DevCodec &d);   // -1 if the codec has no bit-sliced path
-hipError_t launch_bs_encode(int id, const EncodeArgs &a, hipStream_t s);
+// Encode needs a workspace of bs_encode_ws_bytes(ncw) device bytes.
+size_t bs_encode_ws_bytes(size_t ncw);
+hipError_t launch_bs_encode(int id, const EncodeArgs &a, void *ws, hipStream_t s);
 hipError_t launch_bs_syndromes(int id, const DevCodec &d, const DecodeArgs &a, uint8_t *syn_ws,
                                hipStream_t s);
 

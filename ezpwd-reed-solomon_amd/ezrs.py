@@ -62,7 +62,7 @@ def lib():
                                   _vp, _sz, _sz, _vp]
         L.ezrs_encode_host.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _sz, _sz]
         L.ezrs_decode_host.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _vp, _sz, _vp, _vp, _vp,
-                                       _sz, _sz, _sz]
+                                       _sz, _vp, _sz, _sz, _sz]
         L.ezrs_host_alloc.argtypes = [C.POINTER(_vp), _sz]
         L.ezrs_host_free.argtypes = [_vp]
         _lib = L
@@ -181,7 +181,7 @@ class Codec:
                                       chunk), "ezrs_encode_host")
 
     def decode_host(self, data, length=None, parity=None, eras=None, neras=None,
-                    positions=None, chunk=0):
+                    positions=None, corr=None, chunk=0):
         ncw, stride = data.shape
         length = stride - self.nroots if length is None else length
         result = np.zeros(ncw, np.int32)
@@ -189,7 +189,8 @@ class Codec:
             self._h, _np(data), stride, length, _np(parity),
             parity.shape[1] if parity is not None else 0,
             _np(eras), eras.shape[1] if eras is not None else 0, _np(neras), _np(result),
-            _np(positions), positions.shape[1] if positions is not None else 0, ncw, chunk),
+            _np(positions), positions.shape[1] if positions is not None else 0,
+            _np(corr), corr.shape[1] if corr is not None else 0, ncw, chunk),
             "ezrs_decode_host")
         return result
 

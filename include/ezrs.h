@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define EZRS_ABI_VERSION 1
+#define EZRS_ABI_VERSION 2
 
 typedef struct ezrs_codec ezrs_codec;
 
@@ -115,7 +115,8 @@ int ezrs_encode_host(ezrs_codec *codec, const void *data, size_t data_stride, un
 int ezrs_decode_host(ezrs_codec *codec, void *data, size_t data_stride, unsigned len,
                      void *parity, size_t parity_stride, const uint32_t *eras,
                      size_t eras_stride, const uint32_t *neras, int32_t *result,
-                     uint32_t *positions, size_t pos_stride, size_t ncw, size_t chunk);
+                     uint32_t *positions, size_t pos_stride, void *corr, size_t corr_stride,
+                     size_t ncw, size_t chunk);
 
 /* Pinned host memory for the host-memory forms (hipHostMalloc / hipHostFree). */
 int ezrs_host_alloc(void **ptr, size_t bytes);

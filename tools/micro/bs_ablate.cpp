@@ -1,6 +1,7 @@
-// Timing-only ablation driver for the bit-sliced syndrome kernel (RS(255,223), 1M codewords).
-// Built three times: full, -DEZRS_BS_ABLATE_DMA (no HBM stream), -DEZRS_BS_ABLATE_COMPUTE (no XOR
-// networks).  Outputs of the ablated builds are meaningless; only their times matter.
+// Timing-only ablation driver for the bit-sliced kernels (RS(255,223), 1M codewords).
+// Built once per variant: full, -DEZRS_BS_ABLATE_DMA (no HBM stream), -DEZRS_BS_ABLATE_COMPUTE (no
+// XOR networks), -DEZRS_BS_ABLATE_TRANSPOSE (no bit transposition).  Outputs of the ablated builds
+// are meaningless; only their times matter.
 #include "../../ezpwd-reed-solomon_amd/csrc/ezrs_bitslice.hip"
 #include <cstdio>
 #include <vector>
@@ -12,16 +13,21 @@ int main(int argc, char **argv) {
     (void)hipMemset(d, 0x5a, ncw * 255);
     hipEvent_t a, b; (void)hipEventCreate(&a); (void)hipEventCreate(&b);
     const unsigned grid = (unsigned)(ncw / bs::kTile);
-    for (int w = 0; w < 3; ++w)
-        hipLaunchKernelGGL(bs::k_bs_syndromes<bs::BS_RS_255_223>, dim3(grid), dim3(bs::kThreads), 0, 0,
-                           d, (size_t)255, 255u, ncw, (const uint32_t *)nullptr, res, syn);
-    (void)hipEventRecord(a);
     const int it = 20;
-    for (int i = 0; i < it; ++i)
-        hipLaunchKernelGGL(bs::k_bs_syndromes<bs::BS_RS_255_223>, dim3(grid), dim3(bs::kThreads), 0, 0,
-                           d, (size_t)255, 255u, ncw, (const uint32_t *)nullptr, res, syn);
-    (void)hipEventRecord(b); (void)hipEventSynchronize(b);
-    float ms; (void)hipEventElapsedTime(&ms, a, b);
-    printf("%s: %.1f us per launch\n", argc > 1 ? argv[1] : "variant", ms * 1000 / it);
+    for (int which = 0; which < 2; ++which) {
+        for (int i = -3; i < it; ++i) {
+            if (i == 0) (void)hipEventRecord(a);
+            if (which == 0)
+                hipLaunchKernelGGL(bs::k_bs_syndromes<bs::BS_RS_255_223>, dim3(grid), dim3(bs::kThreads), 0, 0,
+                                   d, (size_t)255, 255u, ncw, (const uint32_t *)nullptr, res, syn);
+            else
+                hipLaunchKernelGGL(bs::k_bs_encode<bs::BS_RS_255_223>, dim3(grid), dim3(bs::kThreads), 0, 0,
+                                   d, (size_t)255, 223u, d + 223, (size_t)255, ncw);
+        }
+        (void)hipEventRecord(b); (void)hipEventSynchronize(b);
+        float ms; (void)hipEventElapsedTime(&ms, a, b);
+        printf("%s %s: %.1f us per launch\n", argc > 1 ? argv[1] : "variant",
+               which ? "encode" : "syndromes", ms * 1000 / it);
+    }
     return 0;
 }

@@ -25,11 +25,13 @@ def load(d):
 
 
 def main():
-    d = sys.argv[1]
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    keep_all = "--all" in sys.argv
+    d = args[0]
     res = load(d)
     out = {}
     for k, cs in res.items():
-        if "ezrs" not in k:
+        if "ezrs" not in k and not keep_all:
             continue
         short = k.split("(")[0][-60:]
         o = dict(cs)
@@ -41,8 +43,8 @@ def main():
         print(short)
         for c in sorted(o):
             print(f"   {c:28s} {o[c]:.6g}")
-    if len(sys.argv) > 2:
-        json.dump(out, open(sys.argv[2], "w"), indent=1)
+    if len(args) > 1:
+        json.dump(out, open(args[1], "w"), indent=1)
 
 
 if __name__ == "__main__":
