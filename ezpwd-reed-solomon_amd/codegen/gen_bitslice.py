@@ -2,15 +2,17 @@
 """Generate the constant tables of the bit-sliced GF(2^8) RS kernels (csrc/gen/ezrs_bs_tables.inc).
 
 The kernels evaluate syndromes S_i = r(g_i), g_i = alpha^((fcr+i)*prim) (c++/ezpwd/rs_base:1390-1414),
-on 32 slots per 32-bit register: 8 codewords x 4 interleaved segments (positions p = 4y + s).
-Per segment, Horner in d_i = g_i^4 runs in blocks of 16 y-steps (64 positions):
+on 32 slots per 32-bit register: 4 codewords x 8 interleaved segments (positions p = 8y + sigma).
+Slot bit 8s + k holds codeword k & 3, segment sigma = 4 (k >> 2) + s.  Per segment, Horner in
+d_i = g_i^8 runs in blocks of 16 y-steps (128 positions, one LDS chunk):
 
-    G_i <- G_i * d_i^16 + sum_{t<16} c_{4(16k+t)+s} * d_i^(15-t)
+    G_i <- G_i * d_i^16 + sum_{t<16} c_{8(16k+t)+sigma} * d_i^(15-t)
 
-and the segments are folded with  S_i = g_i^2 (g_i G_0 + G_1) + (g_i G_2 + G_3).  Every constant
-multiplication is a GF(2)-linear 8x8 bit map; the tables below give, for every output bit, the
-4-bit masks of input bits 0-3 and 4-7 it XORs (the kernels precompute all 15 XOR-combinations of
-each input nibble once and spend one v_bitop3 per output bit and input byte).
+and the segments are folded in three levels (x g^4, << 4; x g, << 8; x g^2, << 16), leaving
+S_i = sum_sigma g_i^(7-sigma) G_sigma at bits 28..31.  Every constant multiplication is a
+GF(2)-linear 8x8 bit map; the tables below give, for every output bit, the 4-bit masks of input
+bits 0-3 and 4-7 it XORs (the kernels precompute all 15 XOR-combinations of each input nibble once
+and spend one v_bitop3 per output bit and input byte).
 
 Encode evaluates the data word only and maps the syndromes to parity with the GF(2) matrix Q of
 parity = into_dual?( V^-1 (g^NR * H(data)) ) (see gf8.Codec8.q_rows), in passes of 8 parity
@@ -38,7 +40,14 @@ CODECS = [
 ]
 
 NROLES = 4
-BLOCK = 16     # y-steps per Horner block (an LDS chunk of 128 positions = 2 blocks)
+BLOCK = 16     # y-steps per Horner block (= one LDS chunk of 128 positions)
+SEG = 8        # positions per y-step (segments per codeword slot group)
+
+
+def plane_off(b):
+    """LDS dword offset of bit-plane b from a lane's base (see ezrs_bitslice.hip: the 4 row pieces
+    of a lane sit 64 dwords apart, plane b in row piece b & 3, dword b >> 2 of the y-step)."""
+    return 64 * (b & 3) + (b >> 2)
 
 
 def split(nr):
@@ -105,74 +114,66 @@ def gen_codec(name, poly, fcr, prim, nr, dual):
            f"    static constexpr int S0[{NROLES}] = {{{', '.join(str(a) for a, _ in roles)}}};",
            f"    static constexpr int NS[{NROLES}] = {{{', '.join(str(n) for _, n in roles)}}};",
            f"    static constexpr int NPASS = {npass};   // parity passes of 8 symbols",
-           "    template <int R> static __device__ void block_mul(uint32_t (&S)[16][8]);",
-           "    template <int R, int H> static __device__ void horner_half(uint32_t (&S)[16][8], "
+           "    // s *= d_i^16 (one Horner block) for syndrome S0[R] + I",
+           "    template <int R, int I> static __device__ void mul(uint32_t (&s)[8]);",
+           "    // one Horner block of 16 y-steps",
+           "    template <int R> static __device__ void horner_block(uint32_t (&S)[16][8], "
            "const uint32_t *p);",
-           "    template <int R> static __device__ void fold(uint32_t (&S)[16][8]);",
+           "    // fold the 8 segment partials of syndrome S0[R] + I into bits 28..31",
+           "    template <int R, int I> static __device__ void fold(uint32_t (&s)[8]);",
            "    template <int P> static __device__ void q_pass(uint32_t (&O)[8][8], "
            "const uint32_t *in, int ld);",
            "};"]
-    H = BLOCK // 2
     for r, (r0, n) in enumerate(roles):
         I = "    "
-        # ---- state *= d^BLOCK
-        out.append(f"template <> __device__ __forceinline__ void {st}::block_mul<{r}>(uint32_t (&S)[16][8]) {{")
+        # ---- s *= d^16, one function per syndrome
         for i in range(n):
-            rows = C.mul_rows(gf.pow(gf.pow(C.roots[r0 + i], 4), BLOCK))
-            out.append(f"{I}{{")
-            emit_combos(out, "l", [f"S[{i}][{q}]" for q in range(4)], I + "    ")
-            emit_combos(out, "h", [f"S[{i}][{q}]" for q in range(4, 8)], I + "    ")
+            rows = C.mul_rows(gf.pow(gf.pow(C.roots[r0 + i], SEG), BLOCK))
+            out.append(f"template <> __device__ __forceinline__ void {st}::mul<{r}, {i}>(uint32_t (&s)[8]) {{")
+            emit_combos(out, "l", [f"s[{q}]" for q in range(4)], I)
+            emit_combos(out, "h", [f"s[{q}]" for q in range(4, 8)], I)
             for q in range(8):
-                out.append(f"{I}    " + upd(f"S[{i}][{q}]", None, nib(rows[q])))
-            out.append(f"{I}    __builtin_amdgcn_sched_barrier(0);")
-            out.append(f"{I}}}")
-        out.append("}")
-        # ---- half blocks: y-steps [H*half, H*half + H) of a block, constants d^(BLOCK-1-t)
-        for half in range(2):
-            out.append(f"template <> __device__ __forceinline__ void {st}::horner_half<{r}, {half}>("
-                       "uint32_t (&S)[16][8], const uint32_t *p) {")
-            # bit-planes of y-step t (8 dwords at p[32 b + t]) arrive while y-step t-1 computes
-            out.append(f"{I}uint32_t N[8];")
-            out.append(f"{I}#pragma unroll")
-            out.append(f"{I}for (int b = 0; b < 8; ++b) N[b] = p[32 * b];")
-            for tt in range(H):
-                t = half * H + tt
-                out.append(f"{I}{{ // y-step {t}")
-                out.append(f"{I}    uint32_t P[8];")
-                out.append(f"{I}    #pragma unroll")
-                out.append(f"{I}    for (int b = 0; b < 8; ++b) P[b] = N[b];")
-                if tt + 1 < H:
-                    out.append(f"{I}    #pragma unroll")
-                    out.append(f"{I}    for (int b = 0; b < 8; ++b) N[b] = p[32 * b + {tt + 1}];")
-                out.append(f"{I}    __builtin_amdgcn_sched_barrier(0);")
-                emit_combos(out, "l", ["P[0]", "P[1]", "P[2]", "P[3]"], I + "    ")
-                emit_combos(out, "h", ["P[4]", "P[5]", "P[6]", "P[7]"], I + "    ")
-                for i in range(n):
-                    d = gf.pow(C.roots[r0 + i], 4)
-                    rows = C.input_rows(gf.pow(d, BLOCK - 1 - t))
-                    for q in range(8):
-                        ln = upd(f"S[{i}][{q}]", f"S[{i}][{q}]", nib(rows[q]))
-                        if ln:
-                            out.append(f"{I}    " + ln)
-                out.append(f"{I}    __builtin_amdgcn_sched_barrier(0);")
-                out.append(f"{I}}}")
+                out.append(f"{I}" + upd(f"s[{q}]", None, nib(rows[q])))
             out.append("}")
-        # ---- segment fold
-        out.append(f"template <> __device__ __forceinline__ void {st}::fold<{r}>(uint32_t (&S)[16][8]) {{")
-        for lvl, sh in ((1, 8), (2, 16)):
+        # ---- one block of BLOCK y-steps, constants d^(BLOCK-1-t), straight-line (pad positions
+        # are zero data: from a zero state they leave it zero).  Plane loads are not prefetched
+        # across y-steps: with 4 waves per SIMD the other waves cover the LDS latency, and 8 VGPRs
+        # fewer keep the kernel spill-free at 128.
+        out.append(f"template <> __device__ __forceinline__ void {st}::horner_block<{r}>("
+                   "uint32_t (&S)[16][8], const uint32_t *p) {")
+        for t in range(BLOCK):
+            out.append(f"{I}{{")
+            out.append(f"{I}    uint32_t P[8];")
+            for bb in range(8):
+                out.append(f"{I}    P[{bb}] = p[{plane_off(bb) + 2 * t}];")
+            emit_combos(out, "l", ["P[0]", "P[1]", "P[2]", "P[3]"], I + "    ")
+            emit_combos(out, "h", ["P[4]", "P[5]", "P[6]", "P[7]"], I + "    ")
             for i in range(n):
-                g = C.roots[r0 + i]
-                rows = C.mul_rows(g if lvl == 1 else gf.mul(g, g))
-                out.append(f"{I}{{")
-                emit_combos(out, "l", [f"(S[{i}][{q}] << {sh})" for q in range(4)], I + "    ")
-                emit_combos(out, "h", [f"(S[{i}][{q}] << {sh})" for q in range(4, 8)], I + "    ")
+                d = gf.pow(C.roots[r0 + i], SEG)
+                rows = C.input_rows(gf.pow(d, BLOCK - 1 - t))
                 for q in range(8):
                     ln = upd(f"S[{i}][{q}]", f"S[{i}][{q}]", nib(rows[q]))
                     if ln:
                         out.append(f"{I}    " + ln)
+            out.append(f"{I}    __builtin_amdgcn_sched_barrier(0);")
+            out.append(f"{I}}}")
+        out.append("}")
+        # ---- segment fold, one function per syndrome
+        for i in range(n):
+            g = C.roots[r0 + i]
+            out.append(f"template <> __device__ __forceinline__ void {st}::fold<{r}, {i}>(uint32_t (&s)[8]) {{")
+            for c, sh in ((gf.pow(g, 4), 4), (g, 8), (gf.mul(g, g), 16)):
+                rows = C.mul_rows(c)
+                out.append(f"{I}{{")
+                emit_combos(out, "l", [f"(s[{q}] << {sh})" for q in range(4)], I + "    ")
+                emit_combos(out, "h", [f"(s[{q}] << {sh})" for q in range(4, 8)], I + "    ")
+                for q in range(8):
+                    ln = upd(f"s[{q}]", f"s[{q}]", nib(rows[q]))
+                    if ln:
+                        out.append(f"{I}    " + ln)
                 out.append(f"{I}    __builtin_amdgcn_sched_barrier(0);")
                 out.append(f"{I}}}")
-        out.append("}")
+            out.append("}")
     # ---- encode parity map, one pass of up to 8 parity symbols over full 32-slot registers:
     # O[jl][b] = bit b of parity symbol 8P+jl; in[(8 i + q) * ld] = bit q of syndrome i.
     for P in range(npass):

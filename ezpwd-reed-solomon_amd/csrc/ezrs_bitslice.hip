@@ -6,23 +6,25 @@
 // network; each network is split into nibble groups (all 15 XOR combinations of an input nibble
 // are formed once) and every output bit costs one v_bitop3_b32 (3-input XOR) per input byte.
 //
-// Work decomposition (one 256-thread workgroup = 4 waves = one 512-codeword tile):
-//   * lane l owns the 8 consecutive codewords at tile rows 8l + c, c = 0..7; its 32 register
-//     slots are (c, segment s), s = position mod 4, at bit 8s + c.  Segment interleaving keeps
-//     every step's input a natural little-endian dword of 4 consecutive symbols of one codeword.
-//   * wave r ("role") owns syndromes [S0[r], S0[r]+NS[r]): 8 syndromes x 8 bits = 64 state VGPRs,
-//     so two workgroups (8 waves) share a CU.
-//   * the tile streams through LDS in chunks of 128 positions: lane l's 8 rows x 128 bytes form
-//     block l (pitch 1028 B; the pad dword makes a column read by 32 lanes hit 32 distinct banks).
-//     A block is exactly one LDS-DMA instruction (global_load_lds_dwordx4, 64 lanes x 16 B at
-//     per-lane unaligned row addresses): 128 contiguous bytes per row and request is what lets
-//     the row-strided stream run near HBM speed (tools/micro/dma_patterns.hip).  The other
-//     workgroup on the CU computes while this one waits for its chunk.
-//   * each chunk is bit-transposed once, in place (role r: y-steps 8r..8r+7; 48 ops per 8 dwords),
-//     then every role runs 2 Horner blocks of 16 y-steps in d = g^4 (state *= d^16, then straight-
-//     line XOR networks over the bit-planes, generated from the codec: gen/ezrs_bs_tables.inc).
-//   * the 4 segment partials are folded in-register (x g, << 8; x g^2, << 16), leaving the
-//     syndromes of the lane's 8 codewords in byte lane 3.
+// Work decomposition (one 256-thread workgroup = 4 waves = one 256-codeword tile; 4 workgroups
+// share a CU, so the others compute while one waits for its chunk or sits in a barrier):
+//   * lane l owns the 4 consecutive codewords at tile rows 4l + c, c = 0..3; its 32 register
+//     slots are (c, segment sigma), sigma = position mod 8: slot bit 8s + k holds codeword k & 3,
+//     segment 4 (k >> 2) + s.  Every y-step's input is two natural little-endian dwords (8
+//     consecutive symbols) of each of the lane's 4 codewords.
+//   * wave r ("role") owns syndromes [S0[r], S0[r]+NS[r]): 8 syndromes x 8 bits = 64 state VGPRs.
+//   * the tile streams through LDS in chunks of 128 positions: region m (one LDS-DMA instruction,
+//     global_load_lds_dwordx4, 64 lanes x 16 B at per-lane row addresses; pitch 1028 B) holds the
+//     128-byte row pieces of lanes m and m + 32.  128 contiguous bytes per row and request is what
+//     lets the row-strided stream run fast (tools/micro/dma_patterns.hip: 128-B pieces 4.5 TB/s
+//     latency-bound, 64-B pieces 2.6); a ds_read_b32 half-wave (lanes 0-31 or 32-63) touches each
+//     region once, at bank (m + y) mod 32: conflict-free.
+//   * each chunk is bit-transposed once, in place (role r: y-steps 4r..4r+3; 48 ops per 8 dwords),
+//     then every role runs one Horner block of 16 y-steps in d = g^8 (state *= d^16, then
+//     straight-line XOR networks over the bit-planes, generated from the codec:
+//     gen/ezrs_bs_tables.inc).
+//   * the 8 segment partials are folded in-register (x g^4, << 4; x g, << 8; x g^2, << 16),
+//     leaving the syndromes of the lane's 4 codewords at bits 28..31.
 //
 // Decode (k_bs_syndromes): codewords whose syndromes are all zero (and carry no erasures) get
 // result 0 -- exactly what decode_symbols returns (rs_base:1416-1434); all others get a sentinel
@@ -37,22 +39,29 @@
 namespace ezrs {
 namespace bs {
 
-constexpr int kTile = 512;                 // codewords per workgroup
+constexpr int kTile = 256;                 // codewords per workgroup
 constexpr int kThreads = 256;
 constexpr int kRoles = 4;
-constexpr int kChunk = 128;                // positions per LDS chunk
-constexpr int kBlockDw = 257;              // 8 rows x 32 dwords + 1 pad dword
-constexpr int kBufDw = 64 * kBlockDw;      // one chunk (64 blocks); encode later reuses it for
-                                           // the syndrome exchange (64 x 65 dwords) and the
-                                           // parity image (512 rows x 32 bytes)
-static_assert(kBufDw >= 64 * 65 + kTile * 8, "encode staging does not fit");
+constexpr int kChunk = 128;                // positions per LDS chunk (= one 16-y-step block)
+constexpr int kRegionDw = 257;             // one LDS-DMA region: 8 rows x 32 dwords + 1 pad dword
+constexpr int kBufDw = 32 * kRegionDw;     // one chunk of the tile
+static_assert(kBufDw >= 8 * 32 * (kTile / 32), "encode staging does not fit");
 constexpr int32_t kSentinel = INT32_MIN;
 
 typedef __attribute__((address_space(3))) void lds_void;
 
-// LDS dword index of (lane, slot c, dword y of the chunk) is lane_base + 32 c + y.
-__device__ __forceinline__ int lane_base(int lane) { return lane * kBlockDw; }
-__device__ __forceinline__ int tile_row(int lane, int c) { return 8 * lane + c; }
+// Region m holds rows i = 2c + e (c = 0..3, e = 0..1) = row c of lane m + 32 e, 32 dwords each.
+// Lane l's row c dword t is at lane_base(l) + 64 c + t; after the in-place transposition the
+// dwords 2y, 2y+1 of its 4 rows hold bit-planes b = (row b & 3, dword 2y + (b >> 2)) of y-step y.
+__device__ __forceinline__ int lane_base(int lane) { return (lane & 31) * kRegionDw + 32 * (lane >> 5); }
+__device__ __forceinline__ int tile_row(int lane, int c) { return 4 * lane + c; }
+
+template <int I, int N, class F> __device__ __forceinline__ void static_for(F &&f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
+    }
+}
 
 struct Word {
     const uint8_t *base;   // row 0 of the batch
@@ -61,20 +70,24 @@ struct Word {
     int pad;               // leading zero positions (position = symbol index + pad)
 };
 
-// Issue this wave's 16 LDS-DMA pieces of chunk k: block b = 16*wave + i; lane j fetches row
-// 8b + j/8, bytes [128k - pad + 16 (j&7), +16) of it.  Rows past the batch re-read the last row
-// (discarded); pieces that would start before the batch are clamped (rebuilt by fixup_chunk0).
+// Issue this wave's 8 LDS-DMA pieces of chunk k: region m = 8 wave + i; lane j fetches bytes
+// [128k - pad + 16 (j&7), +16) of region row j >> 3 = 2c + e, i.e. tile row 4 (m + 32 e) + c.
+// Rows past the batch re-read the last row (discarded); pieces that would start before the batch
+// are clamped (rebuilt by fixup_chunk0).
 __device__ __forceinline__ void issue_chunk(uint32_t *buf, const Word &w, int k) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-#pragma unroll 4
-    for (int i = 0; i < 16; ++i) {
-        const int b = 16 * wave + i;
-        size_t cw = w.cw0 + 8 * b + (lane >> 3);
+    const int ri = lane >> 3;                       // region row 2c + e
+    const int rsub = 128 * (ri & 1) + (ri >> 1);    // tile row - 4 m
+    const long col = (long)kChunk * k - w.pad + 16 * (lane & 7);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int m = 8 * wave + i;
+        size_t cw = w.cw0 + 4 * m + rsub;
         if (cw >= w.ncw) cw = w.ncw - 1;
-        long off = (long)(cw * w.stride) + (long)kChunk * k - w.pad + 16 * (lane & 7);
+        long off = (long)(cw * w.stride) + col;
         if (off < 0) off = 0;
         __builtin_amdgcn_global_load_lds(static_cast<const void *>(w.base + off),
-                                         (lds_void *)(buf + b * kBlockDw), 16, 0, 0);
+                                         (lds_void *)(buf + m * kRegionDw), 16, 0, 0);
     }
 }
 
@@ -82,12 +95,12 @@ __device__ __forceinline__ void issue_chunk(uint32_t *buf, const Word &w, int k)
 // was clamped at the start of the batch.
 __device__ __forceinline__ void fixup_chunk0(uint32_t *buf, const Word &w) {
     for (int row = threadIdx.x; row < kTile; row += kThreads) {
-        uint32_t *r = buf + (row >> 3) * kBlockDw + (row & 7) * 32;
+        uint32_t *r = buf + lane_base(row >> 2) + 64 * (row & 3);
         const size_t cw = w.cw0 + row;
         const int nd = (w.pad + 3) >> 2;                  // dwords touched by the pad
         if (cw < w.ncw && (long)(cw * w.stride) < w.pad) {
             const uint8_t *p = w.base + cw * w.stride;
-            for (int d = 0; d < 32; ++d) {
+            for (int d = 0; d < kChunk / 4; ++d) {
                 uint32_t v = 0;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
@@ -106,34 +119,32 @@ __device__ __forceinline__ void fixup_chunk0(uint32_t *buf, const Word &w) {
     }
 }
 
-// In-place bit transposition of this role's 8 y-steps of the chunk: raw dwords (one per row)
-// become bit-planes (plane b of slot (c, s) = bit b of row c's symbol 4y + s).
+// In-place bit transposition of this role's 4 y-steps of the chunk: the 8 raw dwords of a y-step
+// (D[k] = dword 2y + (k >> 2) of row k & 3) become its 8 bit-planes, plane b where D[b] was.
 template <int R>
 __device__ __forceinline__ void transpose_chunk(uint32_t *buf, int lb) {
-#pragma unroll 2
-    for (int t = 0; t < 8; ++t) {
-        uint32_t *p = buf + lb + 8 * R + t;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        uint32_t *p = buf + lb + 2 * (4 * R + t);
         uint32_t D[8];
 #pragma unroll
-        for (int c = 0; c < 8; ++c) D[c] = p[32 * c];
+        for (int k = 0; k < 8; ++k) D[k] = p[64 * (k & 3) + (k >> 2)];
         transpose8(D);
 #pragma unroll
-        for (int b = 0; b < 8; ++b) p[32 * b] = D[b];
+        for (int k = 0; k < 8; ++k) p[64 * (k & 3) + (k >> 2)] = D[k];
     }
 }
 
-// Syndromes (in byte lane 3 after the fold) of the tile's words.  Each role runs its own copy of
+// Syndromes (at bits 28..31 after the fold) of the tile's words.  Each role runs its own copy of
 // the loop (R is a template parameter): with a per-chunk role branch the compiler hoists the
 // common LDS plane loads of all y-steps above the branch and spills.
 template <class C, int R>
 __device__ __forceinline__ void syndromes_tile(uint32_t (&S)[16][8], uint32_t *buf,
                                                const Word &w, int nchunks) {
     const int lb = lane_base(threadIdx.x & 63);
-    // Leading halves of 8 y-steps (32 positions) that hold only pad: Horner over zeros from a
-    // zero state is a no-op, so they are not computed (a shortened word, or encode's 223 symbols
-    // in 2 x 128 positions, skip them).
-    const int skip = w.pad >> 5;
-    bool started = false;
+    // Leading pad positions are zeroed data: Horner over zeros from a zero state is a no-op.  Whole
+    // pad chunks (a heavily shortened word) are not evaluated.
+    const int skip = w.pad / kChunk;
 #pragma unroll
     for (int i = 0; i < 16; ++i)
 #pragma unroll
@@ -153,27 +164,16 @@ __device__ __forceinline__ void syndromes_tile(uint32_t (&S)[16][8], uint32_t *b
 #endif
         __syncthreads();
 #ifndef EZRS_BS_ABLATE_COMPUTE  // timing-only builds: drop the XOR networks
-#pragma unroll 1   // one copy of each role's network: the 4 roles' code must share the I-cache
-        for (int blk = 0; blk < 2; ++blk) {
-            const int h0 = 4 * k + 2 * blk;          // global index of the block's first half
-            if (h0 + 1 < skip) continue;
-            if (started) C::template block_mul<R>(S);
-            const uint32_t *p = buf + lb + 16 * blk;
-            if (h0 >= skip) C::template horner_half<R, 0>(S, p);
-            C::template horner_half<R, 1>(S, p + 8);
-            started = true;
+        if (k >= skip) {
+            if (k > skip) static_for<0, C::NS[R]>([&](auto i) { C::template mul<R, i>(S[i]); });
+            C::template horner_block<R>(S, buf + lb);
         }
 #else
         S[0][0] ^= buf[lb];
 #endif
         __syncthreads();   // the next chunk overwrites the buffer
     }
-    C::template fold<R>(S);
-}
-
-// Byte lane 3 of four registers -> one dword (register a in byte 0).
-__device__ __forceinline__ uint32_t pack4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-    return (a >> 24) | ((b >> 16) & 0xFF00u) | ((c >> 8) & 0xFF0000u) | (d & 0xFF000000u);
+    static_for<0, C::NS[R]>([&](auto i) { C::template fold<R, i>(S[i]); });
 }
 
 template <class C, int R>
@@ -183,29 +183,21 @@ __device__ __forceinline__ uint32_t nonzero_mask(const uint32_t (&S)[16][8]) {
     for (int i = 0; i < C::NS[R]; ++i)
 #pragma unroll
         for (int q = 0; q < 8; ++q) nz |= S[i][q];
-    return nz >> 24;                             // bit c: codeword c has a nonzero syndrome
+    return nz >> 28;                             // bit c: codeword c has a nonzero syndrome
 }
 
-// Write the role's syndromes of the flagged codewords (bits of fl) to their workspace slots.
+// Write the role's syndromes of the flagged codewords (bits of fl) to their workspace slots, one
+// syndrome at a time (after transpose8, S[i][4+c] >> 24 is codeword c's S_i).
 template <class C, int R>
 __device__ __forceinline__ void write_syndromes(uint32_t (&S)[16][8], uint32_t fl, size_t cw0,
                                                 int lane, uint8_t *syn_ws) {
+    uint8_t *dst = syn_ws + (cw0 + tile_row(lane, 0)) * 32 + C::S0[R];
 #pragma unroll
-    for (int i = 0; i < C::NS[R]; ++i) transpose8(S[i]);   // S[i][c] >> 24: codeword c's S_i
+    for (int i = 0; i < C::NS[R]; ++i) {
+        transpose8(S[i]);
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-        if (!(fl >> c & 1)) continue;
-        uint8_t *dst = syn_ws + (cw0 + tile_row(lane, c)) * 32 + C::S0[R];
-#pragma unroll
-        for (int i = 0; i < C::NS[R]; i += 4) {
-            if (i + 4 <= C::NS[R]) {
-                const uint32_t v = pack4(S[i][c], S[i + 1][c], S[i + 2][c], S[i + 3][c]);
-                __builtin_memcpy(dst + i, &v, 4);
-            } else {
-#pragma unroll
-                for (int e = i; e < C::NS[R]; ++e) dst[e] = (uint8_t)(S[e][c] >> 24);
-            }
-        }
+        for (int c = 0; c < 4; ++c)
+            if (fl >> c & 1) dst[32 * c + i] = (uint8_t)(S[i][4 + c] >> 24);
     }
 }
 
@@ -220,18 +212,29 @@ __device__ __forceinline__ void syndromes_body(uint32_t *lds, uint32_t (*flags)[
     flags[R][lane] = nonzero_mask<C, R>(S);
     __syncthreads();
     uint32_t fl = flags[0][lane] | flags[1][lane] | flags[2][lane] | flags[3][lane];
+    int32_t res[4];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
+    for (int c = 0; c < 4; ++c) {
         const size_t cw = w.cw0 + tile_row(lane, c);
-        if (cw >= w.ncw) { fl &= ~(1u << c); continue; }
-        if (neras && neras[cw]) fl |= 1u << c;      // erasures: the error path validates them
-        if (R == 0) result[cw] = (fl >> c & 1) ? kSentinel : 0;
+        if (cw >= w.ncw) fl &= ~(1u << c);
+        else if (neras && neras[cw]) fl |= 1u << c;  // erasures: the error path validates them
+        res[c] = (fl >> c & 1) ? kSentinel : 0;
+    }
+    if (R == 0) {
+        const size_t cw = w.cw0 + tile_row(lane, 0);
+        if (cw + 3 < w.ncw) {
+            __builtin_memcpy(result + cw, res, 16);
+        } else {
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (cw + c < w.ncw) result[cw + c] = res[c];
+        }
     }
     if (fl) write_syndromes<C, R>(S, fl, w.cw0, lane, syn_ws);
 }
 
 template <class C>
-__global__ void __launch_bounds__(kThreads, 2)
+__global__ void __launch_bounds__(kThreads, 4)
     k_bs_syndromes(const uint8_t *data, size_t stride, unsigned nsym, size_t ncw,
                    const uint32_t *neras, int32_t *result, uint8_t *syn_ws) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[kBufDw];
@@ -248,8 +251,9 @@ __global__ void __launch_bounds__(kThreads, 2)
 
 // Encode, stage 1 (k_bs_encode_syn): syndromes of the data words, written to the workspace as
 // bit-planes of 32-codeword groups: dword ((G/64) * 8NR + 8i + q) * 64 + G%64 holds bit q of
-// S_i for codewords 32G .. 32G+31 (bit s <-> codeword 32G + s).  Lane l's byte lane 3 holds
-// codewords 8l .. 8l+7, i.e. byte l&3 of group l>>2's planes: gathered through LDS.
+// S_i for codewords 32G .. 32G+31 (bit s <-> codeword 32G + s).  Lane l's bits 28..31 hold
+// codewords 4l .. 4l+3, i.e. nibble l&7 of group l>>3's planes: pairs of lanes form a byte (DPP),
+// gathered through LDS.
 template <class C, int R>
 __device__ __forceinline__ void encode_syn_body(uint32_t *lds, const Word &w, int nchunks,
                                                 uint32_t *ws) {
@@ -257,22 +261,29 @@ __device__ __forceinline__ void encode_syn_body(uint32_t *lds, const Word &w, in
     uint32_t S[16][8];
     syndromes_tile<C, R>(S, lds, w, nchunks);
     constexpr int NPL = 8 * C::NR;
-    uint8_t *stage = reinterpret_cast<uint8_t *>(lds);     // [NPL planes][16 groups] dwords
+    constexpr int NG = kTile / 32;                         // groups per tile
+    uint8_t *stage = reinterpret_cast<uint8_t *>(lds);     // [NPL planes][NG groups] dwords
 #pragma unroll
     for (int i = 0; i < C::NS[R]; ++i)
 #pragma unroll
-        for (int q = 0; q < 8; ++q)
-            stage[(((C::S0[R] + i) * 8 + q) * 16 + (lane >> 2)) * 4 + (lane & 3)] =
-                (uint8_t)(S[i][q] >> 24);
+        for (int q = 0; q < 8; ++q) {
+            const uint32_t nib = S[i][q] >> 28;
+            // lane l+1's nibble (row_shr:1 within each row of 16 lanes: l odd reads l-1 ... so
+            // even lanes pull their odd neighbour with row_shl:1)
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)nib, 0x101, 0xF, 0xF, false);
+            if (!(lane & 1))
+                stage[(((C::S0[R] + i) * 8 + q) * NG + (lane >> 3)) * 4 + ((lane >> 1) & 3)] =
+                    (uint8_t)(nib | (hi << 4));
+        }
     __syncthreads();
-    const size_t tile = w.cw0 / kTile;
-    uint32_t *dst = ws + (tile >> 2) * NPL * 64 + (tile & 3) * 16;
-    for (int idx = threadIdx.x; idx < NPL * 16; idx += kThreads)
-        dst[(idx >> 4) * 64 + (idx & 15)] = lds[idx];
+    const size_t tile = w.cw0 / kTile;                     // groups 8 tile .. 8 tile + 7
+    uint32_t *dst = ws + (tile >> 3) * NPL * 64 + (tile & 7) * NG;
+    for (int idx = threadIdx.x; idx < NPL * NG; idx += kThreads)
+        dst[(idx / NG) * 64 + (idx % NG)] = lds[idx];
 }
 
 template <class C>
-__global__ void __launch_bounds__(kThreads, 2)
+__global__ void __launch_bounds__(kThreads, 4)
     k_bs_encode_syn(const uint8_t *data, size_t stride, unsigned len, size_t ncw, uint32_t *ws) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[kBufDw];
     const int nchunks = (int)((len + kChunk - 1) / kChunk);
@@ -363,7 +374,7 @@ int bitslice_codec_id(const DevCodec &d) {
 
 size_t bs_encode_ws_bytes(size_t ncw) { return (ncw + 2047) / 2048 * 2048 * 32; }
 
-hipError_t launch_bs_encode(int id, const EncodeArgs &a, void *ws, hipStream_t s) {
+hipError_t launch_bs_encode(int id, const DevCodec &, const EncodeArgs &a, void *ws, hipStream_t s) {
     const unsigned grid = (unsigned)((a.ncw + bs::kTile - 1) / bs::kTile);
     const unsigned pgrid = (unsigned)((a.ncw + 8191) / 8192);   // 256 groups of 32 per block
     uint32_t *w = static_cast<uint32_t *>(ws);

@@ -133,6 +133,8 @@ int ezrs_create(ezrs_codec **out, unsigned symbol_bits, unsigned poly, unsigned 
     d.genpoly = c->d_tabs + 2 * (m.nn + 1);
     d.into_dual = c->d_dual;
     d.from_dual = c->d_dual + 256;
+    if (hipDeviceGetAttribute(&d.ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+        d.ncu = 0;
     c->bs_id = bitslice_codec_id(d);
     *out = c;
     return 0;
@@ -213,7 +215,7 @@ namespace {
 // The one place that picks kernels: every entry point (device or host-memory) goes through these.
 // ws: bs_encode_ws_bytes(ncw) bytes (bit-sliced path only).
 hipError_t dispatch_encode(const ezrs_codec *c, const EncodeArgs &a, void *ws, hipStream_t st) {
-    return c->bs_id >= 0 ? launch_bs_encode(c->bs_id, a, ws, st) : launch_encode_generic(c->dev, a, st);
+    return c->bs_id >= 0 ? launch_bs_encode(c->bs_id, c->dev, a, ws, st) : launch_encode_generic(c->dev, a, st);
 }
 
 // syn_ws: [ncw][32] bytes (bit-sliced path only).

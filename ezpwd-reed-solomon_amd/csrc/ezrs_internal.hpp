@@ -6,6 +6,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <mutex>
+#include <type_traits>
 
 #include "ezrs_field.hpp"
 
@@ -16,6 +17,7 @@ struct DevCodec {
     unsigned mm, nn, nroots, load, fcr, prim, iprim, poly;
     int dual;
     int masked;                   // symbol narrower than its datum (rs_base:1194)
+    int ncu;                      // compute units of the device (persistent grids)
     const uint16_t *alpha_to;     // device, nn+1
     const uint16_t *index_of;     // device, nn+1
     const uint16_t *genpoly;      // device, nroots+1 (index form)
@@ -62,7 +64,7 @@ hipError_t launch_decode_flagged(const DevCodec &c, const DecodeArgs &a, const u
 int bitslice_codec_id(const DevCodec &d);   // -1 if the codec has no bit-sliced path
 // Encode needs a workspace of bs_encode_ws_bytes(ncw) device bytes.
 size_t bs_encode_ws_bytes(size_t ncw);
-hipError_t launch_bs_encode(int id, const EncodeArgs &a, void *ws, hipStream_t s);
+hipError_t launch_bs_encode(int id, const DevCodec &d, const EncodeArgs &a, void *ws, hipStream_t s);
 hipError_t launch_bs_syndromes(int id, const DevCodec &d, const DecodeArgs &a, uint8_t *syn_ws,
                                hipStream_t s);
 

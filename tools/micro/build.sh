@@ -7,6 +7,5 @@ $H -x hip $D/bs_ablate.cpp -o $D/bs_ablate_full &
 $H -x hip -DEZRS_BS_ABLATE_DMA $D/bs_ablate.cpp -o $D/bs_ablate_nodma &
 $H -x hip -DEZRS_BS_ABLATE_COMPUTE $D/bs_ablate.cpp -o $D/bs_ablate_nocomp &
 $H -x hip -DEZRS_BS_ABLATE_TRANSPOSE $D/bs_ablate.cpp -o $D/bs_ablate_notr &
-$H $D/dma_patterns.hip -o $D/dma_patterns &
-$H $D/glds_unaligned.hip -o $D/glds_unaligned &
+$H -x hip -DEZRS_BS_ABLATE_DMA -DEZRS_BS_ABLATE_TRANSPOSE $D/bs_ablate.cpp -o $D/bs_ablate_computeonly &
 wait
