@@ -304,49 +304,78 @@ __device__ __forceinline__ uint32_t gather4(uint32_t a0, uint32_t a1, uint32_t a
     return __builtin_amdgcn_perm(x23, x01, 0x05040100u);
 }
 
+// Encode, stage 2: parity = Q(syndromes) over full 32-codeword registers.  One 256-thread block
+// covers 64 groups (2048 codewords): wave P computes parity symbols 8P..8P+7 of every group (the
+// four waves read the same workspace dwords at the same time: L2 hits), stages them in LDS as
+// [codeword][32] bytes, and the block then writes each codeword's parity as one contiguous run.
+constexpr int kParGroups = 64;                      // groups of 32 codewords per parity block
+constexpr int kParCw = 32 * kParGroups;
+
 template <class C, int P>
-__device__ __forceinline__ void parity_pass(const uint32_t *ws, size_t G, uint8_t *parity,
-                                            size_t pstride, size_t ncw) {
-    constexpr int NPL = 8 * C::NR;
+__device__ __forceinline__ void parity_pass(const uint32_t *ws, size_t G, uint8_t *stage, int g) {
     constexpr int NJ = C::NR - 8 * P < 8 ? C::NR - 8 * P : 8;
     uint32_t O[8][8];
-    C::template q_pass<P>(O, ws + (G >> 6) * NPL * 64 + (G & 63), 64);
+    C::template q_pass<P>(O, ws, 64);
 #pragma unroll
     for (int j = 0; j < NJ; ++j) transpose8(O[j]);   // O[j][c] byte s: symbol 8P+j of cw 32G+8s+c
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < 4; ++s)
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-            const size_t k = 32 * G + 8 * s + c;
-            if (k >= ncw) continue;
-            uint8_t *dst = parity + k * pstride + 8 * P;
+            uint8_t *dst = stage + (32 * g + 8 * s + c) * C::NR + 8 * P;
             if (NJ == 8) {
-                const uint32_t v[2] = {gather4(O[0][c], O[1][c], O[2][c], O[3][c], s),
-                                       gather4(O[4][c], O[5][c], O[6][c], O[7][c], s)};
-                __builtin_memcpy(dst, v, 8);
+                const uint32_t v0 = gather4(O[0][c], O[1][c], O[2][c], O[3][c], s),
+                               v1 = gather4(O[4][c], O[5][c], O[6][c], O[7][c], s);
+                reinterpret_cast<uint32_t *>(dst)[0] = v0;
+                reinterpret_cast<uint32_t *>(dst)[1] = v1;
             } else if (NJ == 4) {
-                const uint32_t v = gather4(O[0][c], O[1][c], O[2][c], O[3][c], s);
-                __builtin_memcpy(dst, &v, 4);
+                reinterpret_cast<uint32_t *>(dst)[0] = gather4(O[0][c], O[1][c], O[2][c], O[3][c], s);
             } else {
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) dst[j] = (uint8_t)(O[j][c] >> (8 * s));
             }
         }
-    }
+    (void)G;
 }
 
-// Encode, stage 2: parity = Q(syndromes) over full 32-codeword registers, one pass of 8 parity
-// symbols per workgroup row (blockIdx.y), 64 groups per wave.
 template <class C>
 __global__ void __launch_bounds__(256)
     k_bs_parity(const uint32_t *ws, uint8_t *parity, size_t pstride, size_t ncw) {
-    const size_t G = ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64 + (threadIdx.x & 63);
-    if (32 * G >= ncw) return;
-    switch (blockIdx.y) {
-    case 0: parity_pass<C, 0>(ws, G, parity, pstride, ncw); break;
-    case 1: if constexpr (C::NPASS > 1) parity_pass<C, 1>(ws, G, parity, pstride, ncw); break;
-    case 2: if constexpr (C::NPASS > 2) parity_pass<C, 2>(ws, G, parity, pstride, ncw); break;
-    default: if constexpr (C::NPASS > 3) parity_pass<C, 3>(ws, G, parity, pstride, ncw); break;
+    __shared__ __attribute__((aligned(16))) uint8_t stage[kParCw * C::NR];
+    const int lane = threadIdx.x & 63;
+    const size_t G = (size_t)blockIdx.x * kParGroups + lane;     // this lane's group
+    const uint32_t *in = ws + (size_t)blockIdx.x * 8 * C::NR * 64 + lane;
+    if (32 * G < ncw) {
+        switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
+        case 0: parity_pass<C, 0>(in, G, stage, lane); break;
+        case 1: if constexpr (C::NPASS > 1) parity_pass<C, 1>(in, G, stage, lane); break;
+        case 2: if constexpr (C::NPASS > 2) parity_pass<C, 2>(in, G, stage, lane); break;
+        default: if constexpr (C::NPASS > 3) parity_pass<C, 3>(in, G, stage, lane); break;
+        }
+    }
+    __syncthreads();
+    // one codeword's NR parity bytes per lane and round: consecutive lanes -> consecutive rows
+    const size_t cw0 = (size_t)blockIdx.x * kParCw;
+    for (int r = threadIdx.x; r < kParCw; r += 256) {
+        const size_t k = cw0 + r;
+        if (k >= ncw) break;
+        uint8_t *dst = parity + k * pstride;
+        const uint8_t *src = stage + r * C::NR;
+        if constexpr (C::NR % 16 == 0) {
+#pragma unroll
+            for (int o = 0; o < C::NR; o += 16) {
+                uint4 v = *reinterpret_cast<const uint4 *>(src + o);
+                __builtin_memcpy(dst + o, &v, 16);
+            }
+        } else if constexpr (C::NR % 4 == 0) {
+#pragma unroll
+            for (int o = 0; o < C::NR; o += 4) {
+                uint32_t v = *reinterpret_cast<const uint32_t *>(src + o);
+                __builtin_memcpy(dst + o, &v, 4);
+            }
+        } else {
+            for (int o = 0; o < C::NR; ++o) dst[o] = src[o];
+        }
     }
 }
 
@@ -376,14 +405,14 @@ size_t bs_encode_ws_bytes(size_t ncw) { return (ncw + 2047) / 2048 * 2048 * 32; 
 
 hipError_t launch_bs_encode(int id, const DevCodec &, const EncodeArgs &a, void *ws, hipStream_t s) {
     const unsigned grid = (unsigned)((a.ncw + bs::kTile - 1) / bs::kTile);
-    const unsigned pgrid = (unsigned)((a.ncw + 8191) / 8192);   // 256 groups of 32 per block
+    const unsigned pgrid = (unsigned)((a.ncw + bs::kParCw - 1) / bs::kParCw);
     uint32_t *w = static_cast<uint32_t *>(ws);
     int k = 0;
 #define EZRS_BS_ENC(C)                                                                            \
     if (k++ == id) {                                                                              \
         hipLaunchKernelGGL(bs::k_bs_encode_syn<bs::C>, dim3(grid), dim3(bs::kThreads), 0, s,      \
                            static_cast<const uint8_t *>(a.data), a.data_stride, a.len, a.ncw, w); \
-        hipLaunchKernelGGL(bs::k_bs_parity<bs::C>, dim3(pgrid, bs::C::NPASS), dim3(256), 0, s,    \
+        hipLaunchKernelGGL(bs::k_bs_parity<bs::C>, dim3(pgrid), dim3(256), 0, s,                  \
                            w, static_cast<uint8_t *>(a.parity), a.parity_stride, a.ncw);          \
         return hipGetLastError();                                                                 \
     }

@@ -26,7 +26,7 @@ int main(int argc, char **argv) {
                 hipLaunchKernelGGL(bs::k_bs_encode_syn<bs::BS_RS_255_223>, dim3(grid), dim3(bs::kThreads), 0, 0,
                                    d, (size_t)255, 223u, ncw, ws);
             else
-                hipLaunchKernelGGL(bs::k_bs_parity<bs::BS_RS_255_223>, dim3((ncw + 8191) / 8192, 4), dim3(256), 0, 0,
+                hipLaunchKernelGGL(bs::k_bs_parity<bs::BS_RS_255_223>, dim3((ncw + bs::kParCw - 1) / bs::kParCw), dim3(256), 0, 0,
                                    ws, d + 223, (size_t)255, ncw);
         }
         (void)hipEventRecord(b); (void)hipEventSynchronize(b);
