@@ -235,3 +235,82 @@ class Ref:
         b = np.zeros(256, np.uint8)
         cls.lib().ezref_dual_tables(_ptr(a), _ptr(b))
         return a, b
+
+
+# ---------------------------------------------------------------------------------------------
+# Binary BCH (oracle/ezbch_oracle.c): the restatement of the Djelic codec behind ezpwd::bch_base
+_bch_ready = False
+
+
+def _bch_lib():
+    global _bch_ready
+    L = lib()
+    if not _bch_ready:
+        L.ezb_create.restype = _vp
+        L.ezb_create.argtypes = [_i, _i, _u]
+        L.ezb_destroy.argtypes = [_vp]
+        L.ezb_info.argtypes = [_vp, _vp]
+        L.ezb_genpoly.argtypes = [_vp, _vp]
+        L.ezb_encode.argtypes = [_vp, _vp, _u, _vp]
+        L.ezb_decode.argtypes = [_vp, _vp, _u, _vp, _vp]
+        L.ezb_correct.argtypes = [_vp, _vp, _u, _vp, _vp]
+        L.ezb_encode_batch.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _sz, _i]
+        L.ezb_decode_batch.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _vp, _vp, _sz, _sz, _i]
+        _bch_ready = True
+    return L
+
+
+class BCH:
+    """BCH codec in the restatement: BCH(m, t, prim_poly=0), i.e. ezpwd::bch_base(m, t, prim_poly)
+    (c++/ezpwd/bch:54-61).  Parity status: pinned by the reference's BCH fixtures only."""
+
+    def __init__(self, m, t, poly=0):
+        L = _bch_lib()
+        self._h = L.ezb_create(m, t, poly)
+        if not self._h:
+            raise ValueError("invalid BCH parameters")
+        info = np.zeros(6, np.uint32)
+        L.ezb_info(self._h, _ptr(info))
+        self.m, self.n, self.t, self.ecc_bits, self.ecc_bytes, self.poly = (int(x) for x in info)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            _bch_lib().ezb_destroy(h)
+            self._h = None
+
+    @property
+    def max_len(self):
+        """Longest data (whole bytes) decode accepts: 8*len <= n - ecc_bits."""
+        return (self.n - self.ecc_bits) // 8
+
+    def genpoly(self):
+        g = np.zeros(self.ecc_bits + 1, np.uint8)
+        _bch_lib().ezb_genpoly(self._h, _ptr(g))
+        return g
+
+    def encode(self, data):
+        data = np.ascontiguousarray(data, np.uint8)
+        ecc = np.zeros(self.ecc_bytes, np.uint8)
+        _bch_lib().ezb_encode(self._h, _ptr(data), len(data), _ptr(ecc))
+        return ecc
+
+    def correct(self, data, ecc):
+        """correct_bch in place on contiguous uint8 arrays; returns (result, error locations)."""
+        loc = np.zeros(2 * self.t + 1, np.uint32)
+        r = _bch_lib().ezb_correct(self._h, _ptr(data), len(data), _ptr(ecc), _ptr(loc))
+        return r, loc[:max(r, 0)].copy()
+
+    def encode_batch(self, data, length, ecc=None, nthreads=1):
+        ncw, stride = data.shape
+        _bch_lib().ezb_encode_batch(self._h, _ptr(data), stride, length, _ptr(ecc),
+                                    ecc.shape[1] if ecc is not None else 0, ncw, nthreads)
+
+    def decode_batch(self, data, length, ecc=None, errloc=None, nthreads=1):
+        ncw, stride = data.shape
+        result = np.zeros(ncw, np.int32)
+        _bch_lib().ezb_decode_batch(self._h, _ptr(data), stride, length, _ptr(ecc),
+                                    ecc.shape[1] if ecc is not None else 0, _ptr(result),
+                                    _ptr(errloc), errloc.shape[1] if errloc is not None else 0,
+                                    ncw, nthreads)
+        return result
