@@ -1,0 +1,757 @@
+// ezbch.hip -- batched binary BCH on MI355X (gfx950) and its C ABI (include/ezbch.h).
+//
+// Semantics: the Djelic / Linux lib/bch.c codec that the reference wraps as ezpwd::bch_base,
+// ezpwd::bch<N,T> and ezpwd::BCH<N,K,T> (c++/ezpwd/bch:48-463) together with ezpwd::correct_bch
+// (c++/ezpwd/bch_base:168-199), applied independently to every codeword of a batch:
+//   encode : ECC = d(x) x^ecc_bits mod g(x), data bits MSB first, ECC left-justified big-endian in
+//            ecc_bytes bytes, zero-initialised (bch:196-205)
+//   decode : decode_bch's result (count / -EBADMSG / -EINVAL) and, as correct_bch, the reported
+//            bits flipped in data and ECC; locations e address data[e/8] bit e%8 (ECC beyond
+//            8*len), reported in ascending order (the reference's order is unpinned).
+//
+// Kernels: one lane per codeword, 256-codeword workgroups.
+//   k_bch_encode    byte-at-a-time LFSR over the data with a left-justified 64-bit remainder and a
+//                   256-entry step table in LDS; each row is read as aligned dwords (v_alignbyte).
+//   k_bch_decode<T> the same remainder XOR the received ECC; zero -> result 0.  Otherwise, in the
+//                   same lane: syndromes S_1..S_2t from the set bits of the difference, binary
+//                   Berlekamp-Massey (odd steps; static register arrays), and the locator's roots:
+//                   degree 1 directly, degrees 2..4 as an affine GF(2)-linear equation
+//                   A4 y^4 + A2 y^2 + A1 y = delta solved by elimination over the m basis bits,
+//                   degree > 4 by a Chien search over the codeword's bit positions.
+// Device limits: t <= 8 and m*t <= 64 (the ECC fits one 64-bit register); other init_bch-valid
+// codecs are refused with -ENOTSUP at creation.  There is no CPU path.
+#include <hip/hip_runtime.h>
+
+#include <cerrno>
+#include <cstdint>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/ezbch.h"
+
+namespace {
+
+constexpr int kMaxT = 8;
+constexpr int kMaxM = 15;
+constexpr int kThreads = 256;
+constexpr int kEBADMSG = 74, kEINVAL = 22;   // Linux errno values, negated as decode_bch returns them
+
+struct DevBch {
+    int m, n, t, ecc_bits, ecc_bytes;
+    int lds_tabs;             // exp/log tables staged in LDS (m <= 12)
+    uint64_t emask;           // the ecc_bits significant bits of a left-justified remainder
+    const uint64_t *step;     // [256] byte-step remainder table
+    const uint16_t *ex;       // [2n] alpha^i
+    const uint16_t *lg;       // [n+1] log_alpha (lg[0] unused)
+};
+
+struct BchArgs {
+    uint8_t *data;
+    size_t dstride;
+    unsigned len;
+    uint8_t *ecc;
+    size_t estride;
+    int32_t *result;
+    uint32_t *errloc;
+    size_t lstride;
+    size_t ncw;
+};
+
+size_t lds_bytes(const DevBch &b, bool tabs) {
+    return 2048 + (tabs && b.lds_tabs ? ((size_t)3 * b.n + 1) * 2 : 0);
+}
+
+// ---- device ------------------------------------------------------------------------------------
+struct GF {
+    const uint16_t *ex, *lg;
+    int n;
+    __device__ uint32_t mul(uint32_t a, uint32_t b) const { return (a && b) ? ex[lg[a] + lg[b]] : 0u; }
+    __device__ uint32_t div(uint32_t a, uint32_t b) const { return a ? ex[lg[a] + n - lg[b]] : 0u; }
+    __device__ uint32_t inv(uint32_t a) const { return ex[n - lg[a]]; }
+    __device__ uint32_t sq(uint32_t a) const { return a ? ex[2 * lg[a]] : 0u; }
+    __device__ uint32_t sqrt(uint32_t a) const {
+        if (!a) return 0u;
+        const uint32_t l = lg[a];
+        return ex[(l & 1) ? (l + n) >> 1 : l >> 1];
+    }
+};
+
+// The bytes p[0..len) in order, read as the aligned dwords that hold them.
+template <class F>
+__device__ __forceinline__ void for_each_byte(const uint8_t *p, unsigned len, F &&f) {
+    if (!len) return;
+    const unsigned a = (unsigned)((uintptr_t)p & 3u);
+    const uint32_t *q = reinterpret_cast<const uint32_t *>(p - a);
+    const unsigned nd = (a + len + 3) >> 2;
+    uint32_t lo = q[0];
+    unsigned i = 0, j = 1;
+    for (; i + 4 <= len; i += 4, ++j) {
+        const uint32_t hi = j < nd ? q[j] : 0u;
+        const uint32_t w = __builtin_amdgcn_alignbyte(hi, lo, a);
+        f(w & 0xffu);
+        f((w >> 8) & 0xffu);
+        f((w >> 16) & 0xffu);
+        f(w >> 24);
+        lo = hi;
+    }
+    if (i < len) {
+        uint32_t w = __builtin_amdgcn_alignbyte(j < nd ? q[j] : 0u, lo, a);
+        for (; i < len; ++i, w >>= 8) f(w & 0xffu);
+    }
+}
+
+__device__ __forceinline__ uint64_t data_remainder(const uint64_t *step, const uint8_t *p,
+                                                   unsigned len) {
+    uint64_t r = 0;
+    for_each_byte(p, len, [&](uint32_t byte) { r = (r << 8) ^ step[(uint32_t)(r >> 56) ^ byte]; });
+    return r;
+}
+
+__device__ __forceinline__ void stage_tables(const DevBch &b, uint8_t *smem, bool tabs) {
+    uint64_t *step = reinterpret_cast<uint64_t *>(smem);
+    for (int i = threadIdx.x; i < 256; i += kThreads) step[i] = b.step[i];
+    if (tabs && b.lds_tabs) {
+        uint16_t *ex = reinterpret_cast<uint16_t *>(smem + 2048), *lg = ex + 2 * b.n;
+        for (int i = threadIdx.x; i < 2 * b.n; i += kThreads) ex[i] = b.ex[i];
+        for (int i = threadIdx.x; i <= b.n; i += kThreads) lg[i] = b.lg[i];
+    }
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(kThreads) k_bch_encode(DevBch b, BchArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    stage_tables(b, smem, false);
+    const size_t k = (size_t)blockIdx.x * kThreads + threadIdx.x;
+    if (k >= a.ncw) return;
+    const uint64_t r = data_remainder(reinterpret_cast<const uint64_t *>(smem),
+                                      a.data + k * a.dstride, a.len);
+    uint8_t *e = a.ecc + k * a.estride;
+    for (int i = 0; i < b.ecc_bytes; ++i) e[i] = (uint8_t)(r >> (56 - 8 * i));
+}
+
+// y -> A4 y^4 + A2 y^2 + A1 y is GF(2)-linear.  With the images of the polynomial-basis vectors
+// 1 << i (= alpha^i) in echelon form: returns the kernel dimension, or -1 if A(y) = delta has no
+// solution; y0 = a particular solution, k1, k2 = the first two kernel basis vectors.
+__device__ int solve_affine(const GF &f, int m, uint32_t A4, uint32_t A2, uint32_t A1,
+                            uint32_t delta, uint32_t &y0, uint32_t &k1, uint32_t &k2) {
+    const int l4 = A4 ? (int)f.lg[A4] : -1, l2 = A2 ? (int)f.lg[A2] : -1, l1 = A1 ? (int)f.lg[A1] : -1;
+    uint32_t v[kMaxM], c[kMaxM];
+    int pb[kMaxM];
+    int dim = 0;
+    k1 = k2 = 0;
+#pragma unroll
+    for (int i = 0; i < kMaxM; ++i) {
+        v[i] = 0;
+        c[i] = 0;
+        pb[i] = -1;
+        if (i < m) {
+            uint32_t w = 0;
+            if (l4 >= 0) w ^= f.ex[l4 + 4 * i];
+            if (l2 >= 0) w ^= f.ex[l2 + 2 * i];
+            if (l1 >= 0) w ^= f.ex[l1 + i];
+            uint32_t cc = 1u << i;
+#pragma unroll
+            for (int k = 0; k < i; ++k)
+                if (pb[k] >= 0 && ((w >> pb[k]) & 1u)) {
+                    w ^= v[k];
+                    cc ^= c[k];
+                }
+            v[i] = w;
+            c[i] = cc;
+            if (w) {
+                pb[i] = 31 - __clz(w);
+            } else {
+                if (dim == 0) k1 = cc;
+                else if (dim == 1) k2 = cc;
+                ++dim;
+            }
+        }
+    }
+    uint32_t y = 0, rem = delta;
+#pragma unroll
+    for (int k = 0; k < kMaxM; ++k)
+        if (pb[k] >= 0 && ((rem >> pb[k]) & 1u)) {
+            rem ^= v[k];
+            y ^= c[k];
+        }
+    y0 = y;
+    return rem ? -1 : dim;
+}
+
+// Roots X of sigma(X) = X^L + a X^(L-1) + b X^(L-2) + c X^(L-3) + d for L = 2..4 (sigma(0) != 0);
+// returns L if there are L distinct roots, else 0.
+__device__ int small_roots(const GF &f, int m, int L, uint32_t a, uint32_t b, uint32_t c, uint32_t d,
+                           uint32_t (&X)[4]) {
+    uint32_t A4, A2, A1, delta, s = 0;
+    int want;                               // kernel dimension of L distinct roots
+    if (L == 2) {                           // y = X:         y^2 + a y = b
+        A4 = 0; A2 = 1; A1 = a; delta = b; want = 1;
+    } else if (L == 3) {                    // y = X + a:     y^4 + (a^2 + b) y^2 + (ab + c) y = 0, y != 0
+        A4 = 1; A2 = f.sq(a) ^ b; A1 = f.mul(a, b) ^ c; delta = 0; want = 2; s = a;
+    } else if (a == 0) {                    // y = X:         y^4 + b y^2 + c y = d
+        A4 = 1; A2 = b; A1 = c; delta = d; want = 2;
+    } else {                                // X = s + 1/y, s^2 = c/a:  y^4 + (as + b)/e y^2 + a/e y = 1/e
+        s = f.sqrt(f.div(c, a));
+        const uint32_t s2 = f.sq(s);
+        const uint32_t e = f.sq(s2) ^ f.mul(a, f.mul(s2, s)) ^ f.mul(b, s2) ^ f.mul(c, s) ^ d;
+        if (!e) return 0;                   // X = s is a double root
+        const uint32_t ie = f.inv(e);
+        A4 = 1; A2 = f.mul(f.mul(a, s) ^ b, ie); A1 = f.mul(a, ie); delta = ie; want = 2;
+    }
+    uint32_t y0, k1, k2;
+    if (solve_affine(f, m, A4, A2, A1, delta, y0, k1, k2) != want) return 0;
+    if (L == 2) {
+        X[0] = y0;
+        X[1] = y0 ^ k1;
+        return 2;
+    }
+    if (L == 3) {                           // y0 = 0: the three nonzero kernel elements
+        X[0] = k1 ^ s;
+        X[1] = k2 ^ s;
+        X[2] = k1 ^ k2 ^ s;
+        return 3;
+    }
+    const uint32_t y[4] = {y0, y0 ^ k1, y0 ^ k2, y0 ^ k1 ^ k2};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) X[i] = a ? f.inv(y[i]) ^ s : y[i];
+    return 4;
+}
+
+// Chien search over the codeword's bit positions p < nbits: X = alpha^p is a root of
+// sigma(X) = sum_j C_j X^(L-j).  Returns the number of roots (their p in P[0..min(cnt,T)).
+template <int T>
+__device__ int chien(const GF &f, const uint32_t (&C)[2 * T + 2], int L, uint32_t nbits,
+                     uint32_t (&P)[T]) {
+    int lt[T + 1];
+#pragma unroll
+    for (int j = 0; j <= T; ++j) lt[j] = (j <= L && C[j]) ? (int)f.lg[C[j]] : -1;
+    int cnt = 0;
+    for (uint32_t p = 0; p < nbits; ++p) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int j = 0; j <= T; ++j)
+            if (lt[j] >= 0) {
+                v ^= f.ex[lt[j]];
+                lt[j] += L - j;
+                if (lt[j] >= f.n) lt[j] -= f.n;
+            }
+        if (!v) {
+#pragma unroll
+            for (int i = 0; i < T; ++i)
+                if (i == cnt) P[i] = p;
+            ++cnt;
+        }
+    }
+    return cnt;
+}
+
+template <int J, int W>
+__device__ __forceinline__ uint32_t coef(const uint32_t (&C)[W]) {
+    if constexpr (J < W) return C[J];
+    else return 0u;
+}
+
+// decode_bch on the masked ECC difference r (left-justified): the count and the ascending error
+// locations, or -EBADMSG.
+template <int T>
+__device__ int locate(const DevBch &b, const GF &f, uint64_t r, uint32_t nbits,
+                      uint32_t (&loc)[T]) {
+    if (!r) return 0;                       // only unused ECC bits differ
+    const uint32_t n = (uint32_t)b.n;
+    uint32_t S[2 * T + 1];
+#pragma unroll
+    for (int j = 0; j <= 2 * T; ++j) S[j] = 0;
+    while (r) {                             // S_j = r(alpha^j), j odd
+        const int lz = __clzll(r);
+        r &= ~(0x8000000000000000ull >> lz);
+        const uint32_t p = (uint32_t)(b.ecc_bits - 1 - lz);
+        uint32_t p2 = 2 * p;
+        if (p2 >= n) p2 -= n;
+        uint32_t e = p;
+#pragma unroll
+        for (int j = 1; j < 2 * T; j += 2) {
+            S[j] ^= f.ex[e];
+            e += p2;
+            if (e >= n) e -= n;
+        }
+    }
+#pragma unroll
+    for (int j = 1; j <= T; ++j) S[2 * j] = f.sq(S[j]);
+
+    // Berlekamp-Massey; for a binary code the even-step discrepancies vanish.  B holds x^m B.
+    constexpr int W = 2 * T + 2;
+    uint32_t C[W], B[W];
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+        C[j] = j == 0;
+        B[j] = j == 1;
+    }
+    int L = 0;
+    uint32_t bd = 1;
+#pragma unroll
+    for (int rr = 1; rr < 2 * T; rr += 2) {
+        uint32_t d = S[rr];
+#pragma unroll
+        for (int i = 1; i < rr; ++i) d ^= f.mul(C[i], S[rr - i]);
+        if (d) {
+            const bool grow = 2 * L <= rr - 1;
+            const uint32_t q = f.div(d, bd);
+            uint32_t old[W];
+#pragma unroll
+            for (int j = 0; j < W; ++j) {
+                old[j] = C[j];
+                C[j] ^= f.mul(q, B[j]);
+            }
+            if (grow) {
+                L = rr - L;
+                bd = d;
+            }
+#pragma unroll
+            for (int j = W - 1; j >= 0; --j) B[j] = j >= 2 ? (grow ? old[j - 2] : B[j - 2]) : 0u;
+        } else {
+#pragma unroll
+            for (int j = W - 1; j >= 0; --j) B[j] = j >= 2 ? B[j - 2] : 0u;
+        }
+    }
+    if (L > T) return -kEBADMSG;
+    if (L == 0) return 0;
+    uint32_t lead = 0;
+#pragma unroll
+    for (int j = 0; j <= T; ++j)
+        if (j == L) lead = C[j];
+    if (!lead) return -kEBADMSG;            // the length exceeds the locator's true degree
+
+    uint32_t P[T];                          // root exponents: X = alpha^P
+    int nr = 0;
+    if (L == 1) {
+        P[0] = f.lg[C[1]];
+        nr = 1;
+    } else if (L <= 4) {
+        uint32_t X[4];
+        nr = small_roots(f, b.m, L, C[1], C[2], coef<3>(C), coef<4>(C), X);
+#pragma unroll
+        for (int i = 0; i < T && i < 4; ++i)
+            if (i < nr) P[i] = f.lg[X[i]];
+    } else {
+        if constexpr (T > 4) nr = chien<T>(f, C, L, nbits, P);
+    }
+    if (nr != L) return -kEBADMSG;
+
+    uint32_t el[T];
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < T; ++i) {
+        el[i] = 0xFFFFFFFFu;
+        if (i < L) {
+            if (P[i] >= nbits) {
+                ok = false;
+            } else {
+                const uint32_t e = nbits - 1 - P[i];
+                el[i] = (e & ~7u) | (7u - (e & 7u));
+            }
+        }
+    }
+    if (!ok) return -kEBADMSG;
+#pragma unroll
+    for (int i = 0; i < T; ++i)
+#pragma unroll
+        for (int j = 0; j + 1 < T - i; ++j) {
+            const uint32_t x = el[j], y = el[j + 1];
+            el[j] = x < y ? x : y;
+            el[j + 1] = x < y ? y : x;
+        }
+#pragma unroll
+    for (int i = 0; i < T; ++i) loc[i] = el[i];
+    return L;
+}
+
+template <int T>
+__global__ void __launch_bounds__(kThreads) k_bch_decode(DevBch b, BchArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    stage_tables(b, smem, true);
+    const size_t k = (size_t)blockIdx.x * kThreads + threadIdx.x;
+    if (k >= a.ncw) return;
+    if (8ull * a.len > (unsigned long long)(b.n - b.ecc_bits)) {   // decode_bch's length check
+        a.result[k] = -kEINVAL;
+        return;
+    }
+    uint8_t *d = a.data + k * a.dstride, *e = a.ecc + k * a.estride;
+    uint64_t r = data_remainder(reinterpret_cast<const uint64_t *>(smem), d, a.len);
+    for (int i = 0; i < b.ecc_bytes; ++i) r ^= (uint64_t)e[i] << (56 - 8 * i);
+    if (!r) {
+        a.result[k] = 0;
+        return;
+    }
+    const uint16_t *sx = reinterpret_cast<const uint16_t *>(smem + 2048);
+    const GF f{b.lds_tabs ? sx : b.ex, b.lds_tabs ? sx + 2 * b.n : b.lg, b.n};
+    uint32_t loc[T];
+    const int cnt = locate<T>(b, f, r & b.emask, 8u * a.len + (uint32_t)b.ecc_bits, loc);
+    a.result[k] = cnt;
+#pragma unroll
+    for (int i = 0; i < T; ++i) {
+        if (i < cnt) {
+            const uint32_t el = loc[i];
+            if (a.errloc) a.errloc[k * a.lstride + i] = el;
+            if (el < 8u * a.len) d[el >> 3] ^= (uint8_t)(1u << (el & 7));
+            else e[(el >> 3) - a.len] ^= (uint8_t)(1u << (el & 7));
+        }
+    }
+}
+
+hipError_t launch_encode(const DevBch &b, const BchArgs &a, hipStream_t s) {
+    const unsigned grid = (unsigned)((a.ncw + kThreads - 1) / kThreads);
+    hipLaunchKernelGGL(k_bch_encode, dim3(grid), dim3(kThreads), lds_bytes(b, false), s, b, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_decode(const DevBch &b, const BchArgs &a, hipStream_t s) {
+    const unsigned grid = (unsigned)((a.ncw + kThreads - 1) / kThreads);
+    const size_t sh = lds_bytes(b, true);
+    switch (b.t) {
+#define EZBCH_CASE(T)                                                                         \
+    case T:                                                                                   \
+        hipLaunchKernelGGL(k_bch_decode<T>, dim3(grid), dim3(kThreads), sh, s, b, a);         \
+        break;
+        EZBCH_CASE(1) EZBCH_CASE(2) EZBCH_CASE(3) EZBCH_CASE(4)
+        EZBCH_CASE(5) EZBCH_CASE(6) EZBCH_CASE(7) EZBCH_CASE(8)
+#undef EZBCH_CASE
+    default:
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// ---- host --------------------------------------------------------------------------------------
+thread_local std::string g_err;
+
+int hip_fail(hipError_t e, const char *what) {
+    g_err = std::string(what) + ": " + hipGetErrorString(e);
+    if (e == hipErrorOutOfMemory) return -ENOMEM;
+    if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return -ENODEV;
+    return -EIO;
+}
+
+#define HIP_TRY(expr)                                          \
+    do {                                                       \
+        hipError_t e_ = (expr);                                \
+        if (e_ != hipSuccess) return hip_fail(e_, #expr);      \
+    } while (0)
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+// init_bch's default primitive polynomials, m = 5..15
+const unsigned kDefaultPoly[11] = {0x25, 0x43, 0x83, 0x11d, 0x211, 0x409,
+                                   0x805, 0x1053, 0x201b, 0x402b, 0x8003};
+
+// Field tables and generator of init_bch(m, t, poly) (bch_base:49-69); false where init_bch fails.
+struct HostBch {
+    unsigned m = 0, n = 0, t = 0, poly = 0, ecc_bits = 0, ecc_bytes = 0;
+    std::vector<uint16_t> ex, lg;
+    std::vector<uint8_t> g;   // generator coefficients, x^0 first
+
+    bool build(unsigned m_, unsigned t_, unsigned poly_) {
+        if (m_ < 5 || m_ > 15) return false;
+        m = m_;
+        n = (1u << m) - 1;
+        t = t_;
+        if (t < 1 || m * t >= n) return false;
+        poly = poly_ ? poly_ : kDefaultPoly[m - 5];
+        if ((poly >> m) != 1) return false;
+        ex.assign(2 * n, 0);
+        lg.assign(n + 1, 0);
+        std::vector<char> seen(n + 1, 0);
+        for (unsigned i = 0, x = 1; i < n; ++i) {
+            if (seen[x]) return false;                  // not primitive
+            seen[x] = 1;
+            ex[i] = ex[i + n] = (uint16_t)x;
+            lg[x] = (uint16_t)i;
+            x <<= 1;
+            if (x >> m) x ^= poly;
+        }
+        std::vector<char> root(n, 0);                   // cyclotomic cosets of 1, 3, .., 2t-1
+        for (unsigned i = 0; i < t; ++i)
+            for (unsigned k = 0, j = 2 * i + 1; k < m; ++k, j = (2 * j) % n) root[j] = 1;
+        std::vector<unsigned> gc(1, 1);
+        auto mul = [&](unsigned a, unsigned b) -> unsigned { return (a && b) ? ex[lg[a] + lg[b]] : 0u; };
+        for (unsigned j = 0; j < n; ++j) {
+            if (!root[j]) continue;
+            const unsigned r = ex[j];
+            gc.push_back(0);
+            for (size_t k = gc.size() - 1; k > 0; --k) gc[k] = gc[k - 1] ^ mul(gc[k], r);
+            gc[0] = mul(gc[0], r);
+        }
+        g.resize(gc.size());
+        for (size_t k = 0; k < gc.size(); ++k) {
+            if (gc[k] > 1) return false;
+            g[k] = (uint8_t)gc[k];
+        }
+        ecc_bits = (unsigned)g.size() - 1;
+        ecc_bytes = (m * t + 7) / 8;
+        return true;
+    }
+
+    // step[v] = (v x^(E+56) mod g) left-justified: the remainder update for one data byte
+    void step_table(uint64_t (&tab)[256]) const {
+        const unsigned E = ecc_bits;
+        uint64_t gl = 0;
+        for (unsigned i = 0; i < E; ++i)
+            if (g[i]) gl |= 1ull << (64 - E + i);
+        for (unsigned v = 0; v < 256; ++v) {
+            uint64_t c = (uint64_t)v << 56;
+            for (int k = 0; k < 8; ++k) c = (c >> 63) ? (c << 1) ^ gl : (c << 1);
+            tab[v] = c;
+        }
+    }
+};
+
+} // namespace
+
+struct ezbch_codec {
+    int device = 0;
+    HostBch h;
+    DevBch dev{};
+    uint64_t *d_step = nullptr;
+    uint16_t *d_tabs = nullptr;
+    std::mutex mu;                // guards the host-pipeline buffers
+    void *d_stage = nullptr;
+    size_t stage_bytes = 0;
+    hipStream_t stream = nullptr;
+};
+
+namespace {
+
+int create_impl(ezbch_codec **out, unsigned m, unsigned t, unsigned poly, int device, long want_k) {
+    if (!out) return -EINVAL;
+    *out = nullptr;
+    HostBch h;
+    if (!h.build(m, t, poly)) {
+        g_err = "init_bch: invalid parameters (need 5 <= m <= 15, t >= 1, m*t < 2^m-1, a primitive "
+                "polynomial of degree m)";
+        return -EINVAL;
+    }
+    if (want_k >= 0 && (long)(h.n - h.ecc_bits) != want_k) {
+        g_err = "BCH<N,K,T>: K does not match the codec init_bch builds (N - ecc_bits)";
+        return -EINVAL;
+    }
+    if (t > (unsigned)kMaxT || m * t > 64) {
+        g_err = "BCH device path supports t <= 8 and m*t <= 64";
+        return -ENOTSUP;
+    }
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev == 0 || device < 0 || device >= ndev) {
+        g_err = "no usable HIP device";
+        return -ENODEV;
+    }
+    ezbch_codec *c = new (std::nothrow) ezbch_codec;
+    if (!c) return -ENOMEM;
+    c->device = device;
+    c->h = std::move(h);
+    DeviceGuard dg(device);
+    uint64_t tab[256];
+    c->h.step_table(tab);
+    const size_t nt = c->h.ex.size() + c->h.lg.size();
+    if ((e = hipMalloc(&c->d_step, sizeof tab)) != hipSuccess ||
+        (e = hipMalloc(&c->d_tabs, nt * sizeof(uint16_t))) != hipSuccess ||
+        (e = hipMemcpy(c->d_step, tab, sizeof tab, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(c->d_tabs, c->h.ex.data(), c->h.ex.size() * 2, hipMemcpyHostToDevice)) !=
+            hipSuccess ||
+        (e = hipMemcpy(c->d_tabs + c->h.ex.size(), c->h.lg.data(), c->h.lg.size() * 2,
+                       hipMemcpyHostToDevice)) != hipSuccess) {
+        ezbch_destroy(c);
+        return hip_fail(e, "BCH tables");
+    }
+    DevBch &d = c->dev;
+    d.m = (int)m;
+    d.n = (int)c->h.n;
+    d.t = (int)t;
+    d.ecc_bits = (int)c->h.ecc_bits;
+    d.ecc_bytes = (int)c->h.ecc_bytes;
+    d.lds_tabs = m <= 12;
+    d.emask = ~0ull << (64 - c->h.ecc_bits);
+    d.step = c->d_step;
+    d.ex = c->d_tabs;
+    d.lg = c->d_tabs + c->h.ex.size();
+    *out = c;
+    return 0;
+}
+
+int check_rows(const ezbch_codec *c, const uint8_t *data, size_t dstride, unsigned len,
+               uint8_t *&ecc, size_t &estride, size_t ncw) {
+    if (!data) return -EINVAL;
+    if (!ecc) {
+        ecc = const_cast<uint8_t *>(data) + len;
+        estride = dstride;
+        if (ncw > 1 && dstride < (size_t)len + c->h.ecc_bytes) return -EINVAL;
+    } else if (ncw > 1 && estride < c->h.ecc_bytes) {
+        return -EINVAL;
+    }
+    if (ncw > 1 && dstride < len) return -EINVAL;
+    return 0;
+}
+
+int ensure_stage(ezbch_codec *c, size_t bytes) {
+    if (!c->stream) HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    if (c->stage_bytes >= bytes) return 0;
+    if (c->d_stage) (void)hipFree(c->d_stage);
+    c->d_stage = nullptr;
+    c->stage_bytes = 0;
+    HIP_TRY(hipMalloc(&c->d_stage, bytes));
+    c->stage_bytes = bytes;
+    return 0;
+}
+
+size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+} // namespace
+
+extern "C" {
+
+const char *ezbch_last_error(void) { return g_err.c_str(); }
+
+int ezbch_create(ezbch_codec **out, unsigned m, unsigned t, unsigned prim_poly, int device) {
+    return create_impl(out, m, t, prim_poly, device, -1);
+}
+
+int ezbch_create_nkt(ezbch_codec **out, unsigned n, unsigned k, unsigned t, int device) {
+    unsigned m = 0;
+    while (m < 16 && ((1u << m) - 1) < n) ++m;
+    if (((1u << m) - 1) != n) {
+        if (out) *out = nullptr;
+        g_err = "BCH<N,K,T>: N must be 2^m - 1";
+        return -EINVAL;
+    }
+    return create_impl(out, m, t, 0, device, (long)k);
+}
+
+int ezbch_destroy(ezbch_codec *c) {
+    if (!c) return 0;
+    DeviceGuard g(c->device);
+    if (c->d_step) (void)hipFree(c->d_step);
+    if (c->d_tabs) (void)hipFree(c->d_tabs);
+    if (c->d_stage) (void)hipFree(c->d_stage);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return 0;
+}
+
+int ezbch_get_info(const ezbch_codec *c, ezbch_info *info) {
+    if (!c || !info) return -EINVAL;
+    info->m = c->h.m;
+    info->n = c->h.n;
+    info->t = c->h.t;
+    info->ecc_bits = c->h.ecc_bits;
+    info->ecc_bytes = c->h.ecc_bytes;
+    info->prim_poly = c->h.poly;
+    info->device = c->device;
+    return 0;
+}
+
+int ezbch_encode(const ezbch_codec *c, const uint8_t *data, size_t data_stride, unsigned len,
+                 uint8_t *ecc, size_t ecc_stride, size_t ncw, void *stream) {
+    if (!c) return -EINVAL;
+    if (ncw == 0) return 0;
+    if (int r = check_rows(c, data, data_stride, len, ecc, ecc_stride, ncw)) return r;
+    DeviceGuard g(c->device);
+    BchArgs a{const_cast<uint8_t *>(data), data_stride, len, ecc, ecc_stride, nullptr, nullptr, 0, ncw};
+    hipError_t e = launch_encode(c->dev, a, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? 0 : hip_fail(e, "BCH encode launch");
+}
+
+int ezbch_decode(const ezbch_codec *c, uint8_t *data, size_t data_stride, unsigned len,
+                 uint8_t *ecc, size_t ecc_stride, int32_t *result, uint32_t *errloc,
+                 size_t errloc_stride, size_t ncw, void *stream) {
+    if (!c) return -EINVAL;
+    if (ncw == 0) return 0;
+    if (!result) return -EINVAL;
+    if (int r = check_rows(c, data, data_stride, len, ecc, ecc_stride, ncw)) return r;
+    if (errloc && ncw > 1 && errloc_stride < c->h.t) return -EINVAL;
+    DeviceGuard g(c->device);
+    BchArgs a{data, data_stride, len, ecc, ecc_stride, result, errloc, errloc_stride, ncw};
+    hipError_t e = launch_decode(c->dev, a, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? 0 : hip_fail(e, "BCH decode launch");
+}
+
+int ezbch_encode_host(ezbch_codec *c, const uint8_t *data, size_t data_stride, unsigned len,
+                      uint8_t *ecc, size_t ecc_stride, size_t ncw, size_t chunk) {
+    if (!c) return -EINVAL;
+    if (ncw == 0) return 0;
+    if (int r = check_rows(c, data, data_stride, len, ecc, ecc_stride, ncw)) return r;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    const size_t eb = c->h.ecc_bytes, row = (size_t)len + eb;
+    if (!chunk) chunk = ((size_t)64 << 20) / row + 1;
+    if (chunk > ncw) chunk = ncw;
+    if (int r = ensure_stage(c, align_up(chunk * row))) return r;
+    uint8_t *st = static_cast<uint8_t *>(c->d_stage);
+    for (size_t k0 = 0; k0 < ncw; k0 += chunk) {
+        const size_t n = ncw - k0 < chunk ? ncw - k0 : chunk;
+        if (len)
+            HIP_TRY(hipMemcpy2DAsync(st, row, data + k0 * data_stride, data_stride, len, n,
+                                     hipMemcpyHostToDevice, c->stream));
+        BchArgs a{st, row, len, st + len, row, nullptr, nullptr, 0, n};
+        HIP_TRY(launch_encode(c->dev, a, c->stream));
+        HIP_TRY(hipMemcpy2DAsync(ecc + k0 * ecc_stride, ecc_stride, st + len, row, eb, n,
+                                 hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    return 0;
+}
+
+int ezbch_decode_host(ezbch_codec *c, uint8_t *data, size_t data_stride, unsigned len,
+                      uint8_t *ecc, size_t ecc_stride, int32_t *result, uint32_t *errloc,
+                      size_t errloc_stride, size_t ncw, size_t chunk) {
+    if (!c) return -EINVAL;
+    if (ncw == 0) return 0;
+    if (!result) return -EINVAL;
+    if (int r = check_rows(c, data, data_stride, len, ecc, ecc_stride, ncw)) return r;
+    if (errloc && errloc_stride < c->h.t) return -EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    const size_t eb = c->h.ecc_bytes, row = (size_t)len + eb, T = c->h.t;
+    if (!chunk) chunk = ((size_t)64 << 20) / row + 1;
+    if (chunk > ncw) chunk = ncw;
+    const size_t b_rows = align_up(chunk * row), b_res = align_up(chunk * 4);
+    if (int r = ensure_stage(c, b_rows + b_res + align_up(errloc ? chunk * T * 4 : 0))) return r;
+    uint8_t *st = static_cast<uint8_t *>(c->d_stage);
+    int32_t *dres = reinterpret_cast<int32_t *>(st + b_rows);
+    uint32_t *dloc = reinterpret_cast<uint32_t *>(st + b_rows + b_res);
+    for (size_t k0 = 0; k0 < ncw; k0 += chunk) {
+        const size_t n = ncw - k0 < chunk ? ncw - k0 : chunk;
+        if (len)
+            HIP_TRY(hipMemcpy2DAsync(st, row, data + k0 * data_stride, data_stride, len, n,
+                                     hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpy2DAsync(st + len, row, ecc + k0 * ecc_stride, ecc_stride, eb, n,
+                                 hipMemcpyHostToDevice, c->stream));
+        if (errloc)   // copy-in/copy-out: entries the decode does not write keep their value
+            HIP_TRY(hipMemcpy2DAsync(dloc, T * 4, errloc + k0 * errloc_stride, errloc_stride * 4,
+                                     T * 4, n, hipMemcpyHostToDevice, c->stream));
+        BchArgs a{st, row, len, st + len, row, dres, errloc ? dloc : nullptr, T, n};
+        HIP_TRY(launch_decode(c->dev, a, c->stream));
+        if (len)
+            HIP_TRY(hipMemcpy2DAsync(data + k0 * data_stride, data_stride, st, row, len, n,
+                                     hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpy2DAsync(ecc + k0 * ecc_stride, ecc_stride, st + len, row, eb, n,
+                                 hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(result + k0, dres, n * 4, hipMemcpyDeviceToHost, c->stream));
+        if (errloc)
+            HIP_TRY(hipMemcpy2DAsync(errloc + k0 * errloc_stride, errloc_stride * 4, dloc, T * 4,
+                                     T * 4, n, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    return 0;
+}
+
+} // extern "C"

@@ -24,6 +24,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libezrs_hip.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "ezrs.h")
+BCH_HEADER = os.path.join(os.path.dirname(HERE), "include", "ezbch.h")
 
 _vp, _sz, _u, _i = C.c_void_p, C.c_size_t, C.c_uint, C.c_int
 
@@ -35,6 +36,11 @@ class EzrsError(RuntimeError):
 class Info(C.Structure):
     _fields_ = [("symbol_bits", _u), ("size", _u), ("nroots", _u), ("load", _u), ("poly", _u),
                 ("fcr", _u), ("prim", _u), ("datum_bytes", _u), ("dual", _i), ("device", _i)]
+
+
+class BCHInfo(C.Structure):
+    _fields_ = [("m", _u), ("n", _u), ("t", _u), ("ecc_bits", _u), ("ecc_bytes", _u),
+                ("prim_poly", _u), ("device", _i)]
 
 
 _lib = None
@@ -65,13 +71,22 @@ def lib():
                                        _sz, _vp, _sz, _sz, _sz]
         L.ezrs_host_alloc.argtypes = [C.POINTER(_vp), _sz]
         L.ezrs_host_free.argtypes = [_vp]
+        L.ezbch_last_error.restype = C.c_char_p
+        L.ezbch_create.argtypes = [C.POINTER(_vp), _u, _u, _u, _i]
+        L.ezbch_create_nkt.argtypes = [C.POINTER(_vp), _u, _u, _u, _i]
+        L.ezbch_destroy.argtypes = [_vp]
+        L.ezbch_get_info.argtypes = [_vp, C.POINTER(BCHInfo)]
+        L.ezbch_encode.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _sz, _vp]
+        L.ezbch_decode.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _vp, _vp, _sz, _sz, _vp]
+        L.ezbch_encode_host.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _sz, _sz]
+        L.ezbch_decode_host.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _vp, _vp, _sz, _sz, _sz]
         _lib = L
     return _lib
 
 
-def _check(rc, what):
+def _check(rc, what, bch=False):
     if rc < 0:
-        msg = lib().ezrs_last_error().decode(errors="replace")
+        msg = (lib().ezbch_last_error() if bch else lib().ezrs_last_error()).decode(errors="replace")
         raise EzrsError(f"{what} failed: {errno.errorcode.get(-rc, rc)} {msg}")
     return rc
 
@@ -195,9 +210,96 @@ class Codec:
         return result
 
 
+class BCH:
+    """A binary BCH codec resident on one HIP device: ezpwd::bch_base(m, t, prim_poly) /
+    ezpwd::BCH<N,K,T> (c++/ezpwd/bch:48-463) over include/ezbch.h.
+
+    * ``encode(data, length, ecc)`` -- bch_base::encode(data, len, parity) per row (bch:196-205)
+    * ``decode(data, length, ecc)`` -- bch_base::decode(data, len, parity, &position), i.e.
+      correct_bch (bch:316-331, bch_base:168-199): int32 result per row, bits fixed in place."""
+
+    def __init__(self, m, t, prim_poly=0, device=0, _h=None):
+        h = _vp()
+        if _h is None:
+            _check(lib().ezbch_create(C.byref(h), m, t, prim_poly, device), "ezbch_create", True)
+        else:
+            h = _h
+        self._h = h
+        info = BCHInfo()
+        _check(lib().ezbch_get_info(self._h, C.byref(info)), "ezbch_get_info", True)
+        self.info = info
+        self.m, self.n, self.t, self.ecc_bits, self.ecc_bytes = (info.m, info.n, info.t,
+                                                                 info.ecc_bits, info.ecc_bytes)
+        self.device = info.device
+
+    @classmethod
+    def nkt(cls, n, k, t, device=0):
+        h = _vp()
+        _check(lib().ezbch_create_nkt(C.byref(h), n, k, t, device), f"ezbch_create_nkt({n},{k},{t})",
+               True)
+        return cls(0, 0, _h=h)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            try:
+                lib().ezbch_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    def __repr__(self):   # bch_base:204-215
+        return f"BCH({self.n},{self.n - self.ecc_bits},{self.t})"
+
+    @property
+    def max_len(self):
+        return (self.n - self.ecc_bits) // 8
+
+    def encode(self, data, length=None, ecc=None, stream=None):
+        """data: [ncw, stride] uint8 device tensor; ecc: [ncw, >=ecc_bytes] or None (the ECC goes
+        to columns length..length+ecc_bytes of data)."""
+        ncw, stride = data.shape
+        length = stride - self.ecc_bytes if length is None else length
+        _check(lib().ezbch_encode(self._h, _tp(data), data.stride(0), length, _tp(ecc),
+                                  ecc.stride(0) if ecc is not None else 0, ncw,
+                                  _stream_ptr(stream)), "ezbch_encode", True)
+
+    def decode(self, data, length=None, ecc=None, result=None, errloc=None, stream=None):
+        import torch
+        ncw, stride = data.shape
+        length = stride - self.ecc_bytes if length is None else length
+        if result is None:
+            result = torch.empty(ncw, dtype=torch.int32, device=data.device)
+        _check(lib().ezbch_decode(self._h, _tp(data), data.stride(0), length, _tp(ecc),
+                                  ecc.stride(0) if ecc is not None else 0, _tp(result),
+                                  _tp(errloc), errloc.stride(0) if errloc is not None else 0, ncw,
+                                  _stream_ptr(stream)), "ezbch_decode", True)
+        return result
+
+    def encode_host(self, data, length=None, ecc=None, chunk=0):
+        ncw, stride = data.shape
+        length = stride - self.ecc_bytes if length is None else length
+        _check(lib().ezbch_encode_host(self._h, _np(data), stride, length, _np(ecc),
+                                       ecc.shape[1] if ecc is not None else 0, ncw, chunk),
+               "ezbch_encode_host", True)
+
+    def decode_host(self, data, length=None, ecc=None, errloc=None, chunk=0):
+        ncw, stride = data.shape
+        length = stride - self.ecc_bytes if length is None else length
+        result = np.zeros(ncw, np.int32)
+        _check(lib().ezbch_decode_host(self._h, _np(data), stride, length, _np(ecc),
+                                       ecc.shape[1] if ecc is not None else 0, _np(result),
+                                       _np(errloc), errloc.shape[1] if errloc is not None else 0,
+                                       ncw, chunk), "ezbch_decode_host", True)
+        return result
+
+
 def exported_symbols():
-    """Function names declared in include/ezrs.h."""
+    """Function names declared in include/ezrs.h and include/ezbch.h."""
     import re
-    txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|void|const char \*|size_t)\s*\*?\s*(ezrs_\w+)\s*\(",
-                                 txt, re.M)))
+    names = set()
+    for fn in (HEADER, BCH_HEADER):
+        txt = open(fn).read()
+        names |= set(re.findall(
+            r"^\s*(?:int|void|const char \*|size_t)\s*\*?\s*(ez(?:rs|bch)_\w+)\s*\(", txt, re.M))
+    return sorted(names)

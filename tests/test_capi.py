@@ -13,7 +13,7 @@ import ezrs
 def test_library_exports_every_declared_symbol():
     L = ezrs.lib()
     declared = ezrs.exported_symbols()
-    assert len(declared) >= 15
+    assert len(declared) >= 24
     for name in declared:
         assert hasattr(L, name), name
     out = subprocess.check_output(["nm", "-D", "--defined-only", ezrs.LIB_PATH], text=True)
@@ -53,3 +53,27 @@ def test_no_device_reports_enodev():
     assert rc == -errno.ENODEV
     with pytest.raises(ezrs.EzrsError):
         ezrs.Codec.rs(255, 223)
+
+
+def test_bch_invalid_codecs_rejected_before_device():
+    L = ezrs.lib()
+    h = C.c_void_p()
+    assert L.ezbch_create(C.byref(h), 4, 1, 0, 0) == -errno.EINVAL          # m < 5
+    assert L.ezbch_create(C.byref(h), 5, 7, 0, 0) == -errno.EINVAL          # m*t >= n
+    assert L.ezbch_create(C.byref(h), 8, 2, 0x101, 0) == -errno.EINVAL      # not primitive
+    assert L.ezbch_create(C.byref(h), 10, 8, 0, 0) == -errno.ENOTSUP        # valid, ECC > 64 bits
+    assert L.ezbch_create_nkt(C.byref(h), 255, 240, 2, 0) == -errno.EINVAL  # BCH<255,240,2> mismatch
+    assert L.ezbch_create_nkt(C.byref(h), 254, 239, 2, 0) == -errno.EINVAL
+    assert not h.value
+    assert L.ezbch_destroy(None) == 0
+    assert L.ezbch_encode(None, None, 0, 1, None, 0, 1, None) == -errno.EINVAL
+
+
+@pytest.mark.skipif(os.environ.get("HIP_VISIBLE_DEVICES") is None and
+                    os.path.exists("/dev/kfd"), reason="a GPU is visible here")
+def test_bch_no_device_reports_enodev():
+    L = ezrs.lib()
+    h = C.c_void_p()
+    assert L.ezbch_create_nkt(C.byref(h), 1023, 983, 4, 0) == -errno.ENODEV
+    with pytest.raises(ezrs.EzrsError):
+        ezrs.BCH(8, 2)
