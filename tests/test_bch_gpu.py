@@ -30,7 +30,7 @@ def _flip(rows, nbits, counts, rng):
 
 
 # (m, t): L <= 4 closed-form roots, L > 4 Chien, LDS and global field tables, unused ECC bits
-CODECS = [(5, 2), (8, 2), (8, 8), (10, 4), (11, 5), (12, 6), (13, 4), (15, 4)]
+CODECS = [(5, 2), (8, 2), (8, 8), (10, 4), (11, 5), (12, 5), (13, 4), (15, 4), (7, 8)]
 
 
 @pytest.mark.parametrize("m,t", CODECS, ids=[f"m{m}t{t}" for m, t in CODECS])
