@@ -108,6 +108,92 @@ def load_traffic(kernel_call):
         return None
 
 
+def bench_c5(args):
+    """C5: BCH(1023,983,4), 1M codewords of 122 data + 5 ECC bytes per GPU.  One step = encode the
+    clean batch + decode a batch carrying 0..4 random bit errors per codeword (restored from a
+    corrupted master copy before each decode; that copy is outside the timed kernels).  value =
+    codeword bytes encoded and decoded per second of kernel time (HIP events), summed over ranks."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import ezrs
+    import shard
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    c = ezrs.BCH.nkt(1023, 983, 4, device=local)
+    ncw, L, row = args.ncw, 122, 127
+    gen = torch.Generator(device="cuda").manual_seed(0x5EED0005 + rank)
+    clean = torch.randint(0, 256, (ncw, row), generator=gen, device="cuda", dtype=torch.int32)
+    clean = clean.to(torch.uint8)
+    c.encode(clean, L)
+    rng = np.random.default_rng(5 + rank)
+    nbits = 8 * L + 40
+    counts = rng.integers(0, 5, ncw)
+    pos = (np.sort(rng.random((ncw, 4)), axis=1) * (nbits - 3)).astype(np.int64) + np.arange(4)
+    bad = clean.cpu().numpy()
+    for j in range(4):
+        r = np.nonzero(counts > j)[0]
+        p = pos[r, j]
+        bad[r, p // 8] ^= (0x80 >> (p % 8)).astype(np.uint8)
+    master = torch.from_numpy(bad).cuda()
+    work = torch.empty_like(master)
+    result = torch.empty(ncw, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream()
+    exp = torch.from_numpy(counts.astype(np.int32)).cuda()
+
+    def step(ev=None):
+        work.copy_(master)
+        if ev:
+            ev[0].record(stream)
+        c.encode(clean, L, stream=stream)
+        if ev:
+            ev[1].record(stream)
+        c.decode(work, L, result=result, stream=stream)
+        if ev:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if not torch.equal(result, exp) or not torch.equal(work, clean):
+        raise SystemExit(f"rank {rank}: C5 decode did not restore the batch")
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    for s in range(args.steps):
+        step(evs[s])
+    torch.cuda.synchronize()
+    enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
+    dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
+    t = shard.max_over_ranks(enc_ms + dec_ms, device="cuda")
+    value = ncw * world * row / (t * 1e-3) / 1e9
+    dom, ms, per = ("ezbch_encode", enc_ms, row) if enc_ms >= dec_ms else ("ezbch_decode", dec_ms, row + 4)
+    achieved = ncw * per / (ms * 1e-3) / 1e9
+    if rank == 0:
+        print(json.dumps({
+            "metric": "BCH(1023,983,4) encode+decode GB/s device-resident (C5)",
+            "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(t, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": "C5: BCH(1023,983,4) encode + decode with 0-4 bit errors, "
+                                   "1M codewords/GPU (restore copy excluded)",
+                       "codewords_per_gpu": ncw, "bytes_per_codeword": row,
+                       "parallelism": f"shard{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": load_traffic(dom), "kernel": dom,
+                         "avg_ms": {"ezbch_encode": round(enc_ms, 4),
+                                    "ezbch_decode": round(dec_ms, 4)}},
+            "cpu_baseline": None}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -117,11 +203,16 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--e2e", action="store_true", help="also time the host-memory pipeline")
+    ap.add_argument("--workload", choices=("c2", "c5"), default="c2",
+                    help="c2: the headline RS(255,223) line; c5: BCH(1023,983,4) (SURVEY.md 8d)")
     args = ap.parse_args()
+    if args.workload == "c5":
+        return bench_c5(args)
 
     import torch
     import torch.distributed as dist
     import ezrs
+    import shard
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -169,10 +260,7 @@ def main():
     elapsed = time.perf_counter() - t0
     enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
     dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = shard.max_over_ranks(elapsed, device="cuda")
 
     total_cw = ncw * world * args.steps
     value = total_cw * N / elapsed / 1e9
