@@ -31,9 +31,9 @@ def main():
     res = load(d)
     out = {}
     for k, cs in res.items():
-        if "ezrs" not in k and not keep_all:
+        if "ezrs" not in k and "bch" not in k and not keep_all:
             continue
-        short = k.split("(")[0][-60:]
+        short = k.replace("(anonymous namespace)::", "").split("(")[0][-60:]
         o = dict(cs)
         if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
             o["hbm_bytes_per_launch"] = (2 * cs["FETCH_SIZE"] + cs["WRITE_SIZE"]) * 1024
