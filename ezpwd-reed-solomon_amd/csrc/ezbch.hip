@@ -58,10 +58,24 @@ struct BchArgs {
     uint32_t *errloc;
     size_t lstride;
     size_t ncw;
+    int staged;               // the block's data rows are copied to LDS with coalesced loads
 };
 
-size_t lds_bytes(const DevBch &b, bool tabs) {
-    return 2048 + (tabs && b.lds_tabs ? ((size_t)3 * b.n + 1) * 2 : 0);
+constexpr size_t kLdsLimit = 65536;
+
+// LDS layout: [0, 2048) byte-step table | exp/log tables (decode, m <= 12) | staged rows
+__host__ __device__ inline size_t rows_offset(const DevBch &b, bool tabs) {
+    return 2048 + (tabs && b.lds_tabs ? (((size_t)3 * b.n + 1) * 2 + 15) / 16 * 16 : 0);
+}
+
+size_t lds_bytes(const DevBch &b, bool tabs, const BchArgs &a) {
+    return rows_offset(b, tabs) + (a.staged ? (size_t)kThreads * a.dstride + 8 : 0);
+}
+
+// Rows are staged when the batch has a row pitch the block's span can hold within 64 KiB of LDS.
+int want_staging(const DevBch &b, bool tabs, const BchArgs &a) {
+    return a.ncw > 1 && a.len > 0 && a.dstride >= a.len &&
+           rows_offset(b, tabs) + (size_t)kThreads * a.dstride + 8 <= kLdsLimit;
 }
 
 // ---- device ------------------------------------------------------------------------------------
@@ -121,13 +135,33 @@ __device__ __forceinline__ void stage_tables(const DevBch &b, uint8_t *smem, boo
     __syncthreads();
 }
 
+// This lane's data row: staged -- the block's rows are one contiguous span of global memory, copied
+// into LDS with coalesced dword loads (a lane-per-row read of 127-byte rows touches a new cache line
+// per lane and load) -- or read in place.
+__device__ __forceinline__ const uint8_t *block_rows(uint8_t *smem, const DevBch &b, bool tabs,
+                                                     const BchArgs &a) {
+    const size_t k0 = (size_t)blockIdx.x * kThreads;
+    if (!a.staged) return a.data + (k0 + threadIdx.x) * a.dstride;
+    const size_t nrows = a.ncw - k0 < (size_t)kThreads ? a.ncw - k0 : (size_t)kThreads;
+    const uint8_t *base = a.data + k0 * a.dstride;
+    const size_t span = (nrows - 1) * a.dstride + a.len;
+    const unsigned off = (unsigned)((uintptr_t)base & 3u);
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(base - off);
+    uint8_t *rows = smem + rows_offset(b, tabs);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(rows);
+    const unsigned nd = (unsigned)((off + span + 3) >> 2);
+    for (unsigned i = threadIdx.x; i < nd; i += kThreads) dst[i] = src[i];
+    __syncthreads();
+    return rows + off + threadIdx.x * a.dstride;
+}
+
 __global__ void __launch_bounds__(kThreads) k_bch_encode(DevBch b, BchArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     stage_tables(b, smem, false);
+    const uint8_t *row = block_rows(smem, b, false, a);
     const size_t k = (size_t)blockIdx.x * kThreads + threadIdx.x;
     if (k >= a.ncw) return;
-    const uint64_t r = data_remainder(reinterpret_cast<const uint64_t *>(smem),
-                                      a.data + k * a.dstride, a.len);
+    const uint64_t r = data_remainder(reinterpret_cast<const uint64_t *>(smem), row, a.len);
     uint8_t *e = a.ecc + k * a.estride;
     for (int i = 0; i < b.ecc_bytes; ++i) e[i] = (uint8_t)(r >> (56 - 8 * i));
 }
@@ -372,6 +406,7 @@ template <int T>
 __global__ void __launch_bounds__(kThreads) k_bch_decode(DevBch b, BchArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     stage_tables(b, smem, true);
+    const uint8_t *row = block_rows(smem, b, true, a);
     const size_t k = (size_t)blockIdx.x * kThreads + threadIdx.x;
     if (k >= a.ncw) return;
     if (8ull * a.len > (unsigned long long)(b.n - b.ecc_bits)) {   // decode_bch's length check
@@ -379,7 +414,7 @@ __global__ void __launch_bounds__(kThreads) k_bch_decode(DevBch b, BchArgs a) {
         return;
     }
     uint8_t *d = a.data + k * a.dstride, *e = a.ecc + k * a.estride;
-    uint64_t r = data_remainder(reinterpret_cast<const uint64_t *>(smem), d, a.len);
+    uint64_t r = data_remainder(reinterpret_cast<const uint64_t *>(smem), row, a.len);
     for (int i = 0; i < b.ecc_bytes; ++i) r ^= (uint64_t)e[i] << (56 - 8 * i);
     if (!r) {
         a.result[k] = 0;
@@ -401,15 +436,17 @@ __global__ void __launch_bounds__(kThreads) k_bch_decode(DevBch b, BchArgs a) {
     }
 }
 
-hipError_t launch_encode(const DevBch &b, const BchArgs &a, hipStream_t s) {
+hipError_t launch_encode(const DevBch &b, BchArgs a, hipStream_t s) {
     const unsigned grid = (unsigned)((a.ncw + kThreads - 1) / kThreads);
-    hipLaunchKernelGGL(k_bch_encode, dim3(grid), dim3(kThreads), lds_bytes(b, false), s, b, a);
+    a.staged = want_staging(b, false, a);
+    hipLaunchKernelGGL(k_bch_encode, dim3(grid), dim3(kThreads), lds_bytes(b, false, a), s, b, a);
     return hipGetLastError();
 }
 
-hipError_t launch_decode(const DevBch &b, const BchArgs &a, hipStream_t s) {
+hipError_t launch_decode(const DevBch &b, BchArgs a, hipStream_t s) {
     const unsigned grid = (unsigned)((a.ncw + kThreads - 1) / kThreads);
-    const size_t sh = lds_bytes(b, true);
+    a.staged = want_staging(b, true, a);
+    const size_t sh = lds_bytes(b, true, a);
     switch (b.t) {
 #define EZBCH_CASE(T)                                                                         \
     case T:                                                                                   \
@@ -665,7 +702,7 @@ int ezbch_encode(const ezbch_codec *c, const uint8_t *data, size_t data_stride, 
     if (ncw == 0) return 0;
     if (int r = check_rows(c, data, data_stride, len, ecc, ecc_stride, ncw)) return r;
     DeviceGuard g(c->device);
-    BchArgs a{const_cast<uint8_t *>(data), data_stride, len, ecc, ecc_stride, nullptr, nullptr, 0, ncw};
+    BchArgs a{const_cast<uint8_t *>(data), data_stride, len, ecc, ecc_stride, nullptr, nullptr, 0, ncw, 0};
     hipError_t e = launch_encode(c->dev, a, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? 0 : hip_fail(e, "BCH encode launch");
 }
@@ -679,7 +716,7 @@ int ezbch_decode(const ezbch_codec *c, uint8_t *data, size_t data_stride, unsign
     if (int r = check_rows(c, data, data_stride, len, ecc, ecc_stride, ncw)) return r;
     if (errloc && ncw > 1 && errloc_stride < c->h.t) return -EINVAL;
     DeviceGuard g(c->device);
-    BchArgs a{data, data_stride, len, ecc, ecc_stride, result, errloc, errloc_stride, ncw};
+    BchArgs a{data, data_stride, len, ecc, ecc_stride, result, errloc, errloc_stride, ncw, 0};
     hipError_t e = launch_decode(c->dev, a, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? 0 : hip_fail(e, "BCH decode launch");
 }
@@ -701,7 +738,7 @@ int ezbch_encode_host(ezbch_codec *c, const uint8_t *data, size_t data_stride, u
         if (len)
             HIP_TRY(hipMemcpy2DAsync(st, row, data + k0 * data_stride, data_stride, len, n,
                                      hipMemcpyHostToDevice, c->stream));
-        BchArgs a{st, row, len, st + len, row, nullptr, nullptr, 0, n};
+        BchArgs a{st, row, len, st + len, row, nullptr, nullptr, 0, n, 0};
         HIP_TRY(launch_encode(c->dev, a, c->stream));
         HIP_TRY(hipMemcpy2DAsync(ecc + k0 * ecc_stride, ecc_stride, st + len, row, eb, n,
                                  hipMemcpyDeviceToHost, c->stream));
@@ -738,7 +775,7 @@ int ezbch_decode_host(ezbch_codec *c, uint8_t *data, size_t data_stride, unsigne
         if (errloc)   // copy-in/copy-out: entries the decode does not write keep their value
             HIP_TRY(hipMemcpy2DAsync(dloc, T * 4, errloc + k0 * errloc_stride, errloc_stride * 4,
                                      T * 4, n, hipMemcpyHostToDevice, c->stream));
-        BchArgs a{st, row, len, st + len, row, dres, errloc ? dloc : nullptr, T, n};
+        BchArgs a{st, row, len, st + len, row, dres, errloc ? dloc : nullptr, T, n, 0};
         HIP_TRY(launch_decode(c->dev, a, c->stream));
         if (len)
             HIP_TRY(hipMemcpy2DAsync(data + k0 * data_stride, data_stride, st, row, len, n,
