@@ -108,6 +108,106 @@ def load_traffic(kernel_call):
         return None
 
 
+def bench_rs_errors(args):
+    """C3: RS(255,223), 1M codewords, each with 12 corrupted symbols of which the last 4 are passed as
+    erasures (exercise.H:174-177); C4: RS(65535,65503), 4096 codewords (--ncw; 65536 is the full
+    config), same corruption.  One step = encode the clean batch + decode a corrupted copy (restored
+    from a master before each decode, outside the timed kernels).  value = codeword bytes encoded
+    and decoded per second of kernel time (HIP events), summed over ranks."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import ezrs
+    import shard
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    c3 = args.workload == "c3"
+    n, k = (255, 223) if c3 else (65535, 65503)
+    ncw = args.ncw if (c3 or args.ncw != 1 << 20) else 4096
+    c = ezrs.Codec.rs(n, k, device=local)
+    c.reserve(ncw)
+    w = 1 if c3 else 2
+    rng = np.random.default_rng(0x5EED0003 + rank)
+    host = rng.integers(0, n + 1, (ncw, n)).astype(np.uint8 if c3 else np.uint16)
+    tdt = torch.uint8 if c3 else torch.int16
+    clean = torch.from_numpy(host.view(np.int16) if not c3 else host).cuda()
+    if not c3:
+        clean = clean.view(torch.uint16)
+    c.encode(clean, k)
+    torch.cuda.synchronize()
+    enc = clean.view(tdt).cpu().numpy().view(host.dtype)
+    bad = enc.copy()
+    eras = np.zeros((ncw, 32), np.uint32)
+    rows = np.arange(ncw)[:, None]
+    locs = np.argsort(rng.random((ncw, n)), axis=1)[:, :12] if c3 else \
+        np.stack([rng.choice(n, 12, replace=False) for _ in range(ncw)])
+    bad[rows, locs] ^= rng.integers(1, n + 1, (ncw, 12)).astype(host.dtype)
+    eras[:, :4] = locs[:, 8:]
+    master = torch.from_numpy(bad.view(np.int16) if not c3 else bad).cuda()
+    work = torch.empty_like(master)
+    d_eras = torch.from_numpy(eras.view(np.int32)).cuda()
+    d_neras = torch.full((ncw,), 4, dtype=torch.int32, device="cuda")
+    result = torch.empty(ncw, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream()
+
+    def view(t):
+        return t if c3 else t.view(torch.uint16)
+
+    def step(ev=None):
+        work.copy_(master)
+        if ev:
+            ev[0].record(stream)
+        c.encode(view(clean), k, stream=stream)
+        if ev:
+            ev[1].record(stream)
+        c.decode(view(work), k, eras=d_eras, neras=d_neras, result=result, stream=stream)
+        if ev:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if not bool((result == 12).all()) or not torch.equal(work, clean.view(work.dtype)):
+        raise SystemExit(f"rank {rank}: {args.workload} decode did not restore the batch")
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    for s_ in range(args.steps):
+        step(evs[s_])
+    torch.cuda.synchronize()
+    enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
+    dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
+    t = shard.max_over_ranks(enc_ms + dec_ms, device="cuda")
+    row = n * w
+    value = ncw * world * row / (t * 1e-3) / 1e9
+    dom, ms, per = ("ezrs_encode", enc_ms, row) if enc_ms >= dec_ms else ("ezrs_decode", dec_ms, row + 4)
+    achieved = ncw * per / (ms * 1e-3) / 1e9
+    if rank == 0:
+        print(json.dumps({
+            "metric": f"RS({n},{k}) encode + 8-error/4-erasure decode GB/s device-resident "
+                      f"({args.workload.upper()})",
+            "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(t, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8" if c3 else "u16",
+            "data": "synthetic",
+            "config": {"workload": f"{args.workload.upper()}: RS({n},{k}) encode + decode of 8 errors "
+                                   f"+ 4 erasures per codeword (restore copy excluded)",
+                       "codewords_per_gpu": ncw, "bytes_per_codeword": row,
+                       "parallelism": f"shard{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": None, "kernel": dom,
+                         "avg_ms": {"ezrs_encode": round(enc_ms, 4), "ezrs_decode": round(dec_ms, 4)}},
+            "cpu_baseline": None}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def bench_c5(args):
     """C5: BCH(1023,983,4), 1M codewords of 122 data + 5 ECC bytes per GPU.  One step = encode the
     clean batch + decode a batch carrying 0..4 random bit errors per codeword (restored from a
@@ -203,11 +303,14 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--e2e", action="store_true", help="also time the host-memory pipeline")
-    ap.add_argument("--workload", choices=("c2", "c5"), default="c2",
-                    help="c2: the headline RS(255,223) line; c5: BCH(1023,983,4) (SURVEY.md 8d)")
+    ap.add_argument("--workload", choices=("c2", "c3", "c4", "c5"), default="c2",
+                    help="c2: the headline RS(255,223) line; c3: RS(255,223) 8 errors + 4 erasures "
+                         "decode; c4: RS(65535,65503); c5: BCH(1023,983,4) (SURVEY.md 8d)")
     args = ap.parse_args()
     if args.workload == "c5":
         return bench_c5(args)
+    if args.workload in ("c3", "c4"):
+        return bench_rs_errors(args)
 
     import torch
     import torch.distributed as dist

@@ -297,24 +297,40 @@ __global__ void __launch_bounds__(kBlock) k_decode_generic(DevCodec c, DecodeArg
 
 constexpr int32_t kSentinel = INT32_MIN;
 
+// Each thread screens kFlagPer consecutive results (one 16-byte load): a clean batch -- the common
+// case -- costs a quarter of the blocks of a thread-per-codeword screen.
+constexpr int kFlagPer = 4;
+
 __global__ void __launch_bounds__(kBlock) k_decode_flagged(DevCodec c, DecodeArgs a,
                                                            const uint8_t *syn_ws) {
     __shared__ __attribute__((aligned(16))) uint16_t smem[2 * 256 + 256];
-    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool mine = k < a.ncw && a.result[k] == kSentinel;
-    if (!__syncthreads_or(mine)) return;     // the common case: a clean block leaves at once
+    const size_t k0 = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * kFlagPer;
+    unsigned mine = 0;
+    if (k0 + kFlagPer <= a.ncw && (reinterpret_cast<uintptr_t>(a.result + k0) & 15) == 0) {
+        int4 r;
+        __builtin_memcpy(&r, a.result + k0, 16);
+        mine = (r.x == kSentinel) | (r.y == kSentinel) << 1 | (r.z == kSentinel) << 2 |
+               (r.w == kSentinel) << 3;
+    } else {
+        for (int i = 0; i < kFlagPer; ++i)
+            if (k0 + i < a.ncw && a.result[k0 + i] == kSentinel) mine |= 1u << i;
+    }
+    if (!__syncthreads_or(mine != 0)) return;     // the common case: a clean block leaves at once
     const uint16_t *A, *I;
     const uint8_t *ID, *FD;
     stage_tables<true>(c, smem, A, I, ID, FD);
-    if (!mine) return;
-    uint8_t *data = static_cast<uint8_t *>(a.data) + k * a.data_stride;
-    uint8_t *parity = static_cast<uint8_t *>(a.parity) + k * a.parity_stride;
-    const uint32_t *eras = a.eras ? a.eras + k * a.eras_stride : nullptr;
-    const unsigned ne = a.neras ? a.neras[k] : 0;
-    uint32_t *pos = a.positions ? a.positions + k * a.pos_stride : nullptr;
-    uint8_t *corr = a.corr ? static_cast<uint8_t *>(a.corr) + k * a.corr_stride : nullptr;
-    a.result[k] = decode_one<uint8_t, 32>(c, A, I, ID, FD, data, a.len, parity, eras, ne, pos,
-                                          corr, syn_ws + k * 32);
+    for (int i = 0; i < kFlagPer; ++i) {
+        if (!(mine >> i & 1)) continue;
+        const size_t k = k0 + i;
+        uint8_t *data = static_cast<uint8_t *>(a.data) + k * a.data_stride;
+        uint8_t *parity = static_cast<uint8_t *>(a.parity) + k * a.parity_stride;
+        const uint32_t *eras = a.eras ? a.eras + k * a.eras_stride : nullptr;
+        const unsigned ne = a.neras ? a.neras[k] : 0;
+        uint32_t *pos = a.positions ? a.positions + k * a.pos_stride : nullptr;
+        uint8_t *corr = a.corr ? static_cast<uint8_t *>(a.corr) + k * a.corr_stride : nullptr;
+        a.result[k] = decode_one<uint8_t, 32>(c, A, I, ID, FD, data, a.len, parity, eras, ne, pos,
+                                              corr, syn_ws + k * 32);
+    }
 }
 
 template <typename T, int MAXR>
@@ -346,7 +362,8 @@ hipError_t dec_launch(const DevCodec &c, const DecodeArgs &a, hipStream_t s) {
 hipError_t launch_decode_flagged(const DevCodec &c, const DecodeArgs &a, const uint8_t *syn_ws,
                                  hipStream_t s) {
     if (a.ncw == 0) return hipSuccess;
-    const unsigned grid = (unsigned)((a.ncw + kBlock - 1) / kBlock);
+    const size_t per = (size_t)kBlock * kFlagPer;
+    const unsigned grid = (unsigned)((a.ncw + per - 1) / per);
     hipLaunchKernelGGL(k_decode_flagged, dim3(grid), dim3(kBlock), 0, s, c, a, syn_ws);
     return hipGetLastError();
 }
