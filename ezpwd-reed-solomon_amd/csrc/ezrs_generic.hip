@@ -97,12 +97,16 @@ __global__ void __launch_bounds__(kBlock) k_encode_generic(DevCodec c, EncodeArg
 // decode_symbols on one codeword.  Corrections are recorded and applied at the end: for the direct
 // path every recorded correction (the reference corrects in place, so partial corrections before a
 // failure persist, rs_base:1238-1241), for the masked path only when count > 0 (rs_base:1223-1234).
-template <typename T, int MAXR>
+// Working arrays: private (WS = 0), or -- for the flagged-codeword kernel, whose per-lane arrays
+// with data-dependent indices would otherwise sit in waterfall-indexed VGPRs -- in LDS at `lds`,
+// element i of a lane's array at lds[i * WS] (lanes interleaved: conflict-free).  W is the element
+// type: uint16_t, or uint8_t where every value fits (m = 8: indices, log values and A0 = 255).
+template <typename T, int MAXR, int WS = 0, typename W = uint16_t>
 __device__ int decode_one(const DevCodec &c, const uint16_t *__restrict__ A,
                           const uint16_t *__restrict__ I, const uint8_t *ID, const uint8_t *FD,
                           T *data, unsigned len, T *parity, const uint32_t *eras,
                           unsigned no_eras, uint32_t *pos_out, T *corr_out,
-                          const uint8_t *syn_in = nullptr) {
+                          const uint8_t *syn_in = nullptr, W *lds = nullptr) {
     const unsigned NR = c.nroots, NN = c.nn, A0 = c.nn, mm = c.mm, LOAD = c.load;
     const unsigned FCR = c.fcr, PRM = c.prim;
     if (len == 0 || len > LOAD) return -1;                                    // 1375-1377
@@ -114,10 +118,14 @@ __device__ int decode_one(const DevCodec &c, const uint16_t *__restrict__ A,
             if (static_cast<unsigned>(parity[i]) & ~NN) return -1;            // 1215-1218
     const unsigned pad = LOAD - len;
 
-    uint16_t syn[MAXR], lambda[MAXR + 1], b[MAXR + 1], t[MAXR + 1], omega[MAXR + 1];
-    uint16_t root[MAXR], loc[MAXR], fixv[MAXR], corrv[MAXR];
-    uint16_t fixp[MAXR];
-    uint8_t wrote[MAXR];              // corr[j] written by the reference's Forney loop
+    constexpr int kS = WS ? WS : 1;
+    constexpr int kW = MAXR + 1;       // elements per working array
+    W priv[WS ? 1 : 11 * kW];
+    W *const base = WS ? lds : priv;
+    W *syn = base, *lambda = base + kW * kS, *b = base + 2 * kW * kS, *t = base + 3 * kW * kS,
+             *omega = base + 4 * kW * kS, *root = base + 5 * kW * kS, *loc = base + 6 * kW * kS,
+             *fixv = base + 7 * kW * kS, *corrv = base + 8 * kW * kS, *fixp = base + 9 * kW * kS,
+             *wrote = base + 10 * kW * kS;   // wrote: corr[j] written by the reference's Forney loop
     unsigned nfix = 0, nroot = 0;
     int count = 0;
     unsigned deg_lambda = 0, deg_omega = 0, r = no_eras, el = no_eras;
@@ -129,124 +137,124 @@ __device__ int decode_one(const DevCodec &c, const uint16_t *__restrict__ A,
     // syndromes by Horner over data then parity (1390-1414), unless the bit-sliced kernel
     // already evaluated them (same values: S_i = r(alpha^((fcr+i)*prim)) in polynomial form)
     if (syn_in) {
-        for (unsigned i = 0; i < NR; ++i) syn[i] = syn_in[i];
+        for (unsigned i = 0; i < NR; ++i) syn[(i) * kS] = syn_in[i];
     } else {
         const unsigned s0 = cnv(data[0]);
-        for (unsigned i = 0; i < NR; ++i) syn[i] = (uint16_t)s0;
+        for (unsigned i = 0; i < NR; ++i) syn[(i) * kS] = (uint16_t)s0;
         for (unsigned j = 1; j < len + NR; ++j) {
             const unsigned x = cnv(j < len ? static_cast<unsigned>(data[j])
                                            : static_cast<unsigned>(parity[j - len]));
             for (unsigned i = 0; i < NR; ++i)
-                syn[i] = syn[i] == 0 ? (uint16_t)x
-                                     : (uint16_t)(x ^ A[modnn(I[syn[i]] + (FCR + i) * PRM, NN, mm)]);
+                syn[(i) * kS] = syn[(i) * kS] == 0 ? (uint16_t)x
+                                     : (uint16_t)(x ^ A[modnn(I[syn[(i) * kS]] + (FCR + i) * PRM, NN, mm)]);
         }
     }
     unsigned syn_error = 0;
     for (unsigned i = 0; i < NR; ++i) {
-        syn_error |= syn[i];
-        syn[i] = I[syn[i]];
+        syn_error |= syn[(i) * kS];
+        syn[(i) * kS] = I[syn[(i) * kS]];
     }
     if (!syn_error) return 0;                                                 // 1427-1434
 
-    for (unsigned i = 0; i <= NR; ++i) lambda[i] = 0;                        // 1436-1450
-    lambda[0] = 1;
+    for (unsigned i = 0; i <= NR; ++i) lambda[(i) * kS] = 0;                        // 1436-1450
+    lambda[(0) * kS] = 1;
     if (no_eras > 0) {
-        lambda[1] = A[modnn(PRM * (NN - 1 - (eras[0] + pad)), NN, mm)];
+        lambda[(1) * kS] = A[modnn(PRM * (NN - 1 - (eras[0] + pad)), NN, mm)];
         for (unsigned i = 1; i < no_eras; ++i) {
             const unsigned u = modnn(PRM * (NN - 1 - (eras[i] + pad)), NN, mm);
             for (unsigned j = i + 1; j > 0; --j) {
-                const unsigned tmp = I[lambda[j - 1]];
-                if (tmp != A0) lambda[j] ^= A[modnn(u + tmp, NN, mm)];
+                const unsigned tmp = I[lambda[(j - 1) * kS]];
+                if (tmp != A0) lambda[(j) * kS] ^= A[modnn(u + tmp, NN, mm)];
             }
         }
     }
-    for (unsigned i = 0; i <= NR; ++i) b[i] = I[lambda[i]];
+    for (unsigned i = 0; i <= NR; ++i) b[(i) * kS] = I[lambda[(i) * kS]];
 
     while (++r <= NR) {                                                       // BM 1507-1546
         unsigned discr_r = 0;
         for (unsigned i = 0; i < r; ++i)
-            if (lambda[i] != 0 && syn[r - i - 1] != A0)
-                discr_r ^= A[modnn(I[lambda[i]] + syn[r - i - 1], NN, mm)];
+            if (lambda[(i) * kS] != 0 && syn[(r - i - 1) * kS] != A0)
+                discr_r ^= A[modnn(I[lambda[(i) * kS]] + syn[(r - i - 1) * kS], NN, mm)];
         discr_r = I[discr_r];
         if (discr_r == A0) {
-            for (unsigned i = NR; i > 0; --i) b[i] = b[i - 1];
-            b[0] = (uint16_t)A0;
+            for (unsigned i = NR; i > 0; --i) b[(i) * kS] = b[(i - 1) * kS];
+            b[(0) * kS] = (uint16_t)A0;
         } else {
-            t[0] = lambda[0];
+            t[(0) * kS] = lambda[(0) * kS];
             for (unsigned i = 0; i < NR; ++i)
-                t[i + 1] = b[i] != A0 ? (uint16_t)(lambda[i + 1] ^ A[modnn(discr_r + b[i], NN, mm)])
-                                      : lambda[i + 1];
+                t[(i + 1) * kS] = b[(i) * kS] != A0 ? (uint16_t)(lambda[(i + 1) * kS] ^ A[modnn(discr_r + b[(i) * kS], NN, mm)])
+                                      : lambda[(i + 1) * kS];
             if (2 * el <= r + no_eras - 1) {
                 el = r + no_eras - el;
                 for (unsigned i = 0; i <= NR; ++i)
-                    b[i] = lambda[i] == 0 ? (uint16_t)A0
-                                          : (uint16_t)modnn(I[lambda[i]] - discr_r + NN, NN, mm);
+                    b[(i) * kS] = lambda[(i) * kS] == 0 ? (uint16_t)A0
+                                          : (uint16_t)modnn(I[lambda[(i) * kS]] - discr_r + NN, NN, mm);
             } else {
-                for (unsigned i = NR; i > 0; --i) b[i] = b[i - 1];
-                b[0] = (uint16_t)A0;
+                for (unsigned i = NR; i > 0; --i) b[(i) * kS] = b[(i - 1) * kS];
+                b[(0) * kS] = (uint16_t)A0;
             }
-            for (unsigned i = 0; i <= NR; ++i) lambda[i] = t[i];
+            for (unsigned i = 0; i <= NR; ++i) lambda[(i) * kS] = t[(i) * kS];
         }
     }
 
     for (unsigned i = 0; i <= NR; ++i) {                                      // 1549-1553
-        lambda[i] = I[lambda[i]];
-        if (lambda[i] != NN) deg_lambda = i;
+        lambda[(i) * kS] = I[lambda[(i) * kS]];
+        if (lambda[(i) * kS] != NN) deg_lambda = i;
     }
     {                                                                         // Chien 1555-1584
-        uint16_t *reg = t;
-        for (unsigned i = 0; i <= NR; ++i) reg[i] = lambda[i];
+        W *reg = t;
+        for (unsigned i = 0; i <= NR; ++i) reg[(i) * kS] = lambda[(i) * kS];
         count = 0;
         for (unsigned i = 1, k = c.iprim - 1; i <= NN; ++i, k = modnn(k + c.iprim, NN, mm)) {
             unsigned q = 1;
             for (unsigned j = deg_lambda; j > 0; --j)
-                if (reg[j] != A0) {
-                    reg[j] = (uint16_t)modnn(reg[j] + j, NN, mm);
-                    q ^= A[reg[j]];
+                if (reg[(j) * kS] != A0) {
+                    reg[(j) * kS] = (uint16_t)modnn(reg[(j) * kS] + j, NN, mm);
+                    q ^= A[reg[(j) * kS]];
                 }
             if (q != 0) continue;
-            root[count] = (uint16_t)i;
-            loc[count] = (uint16_t)k;
+            root[(count) * kS] = (uint16_t)i;
+            loc[(count) * kS] = (uint16_t)k;
             if (++count == (int)deg_lambda) break;
         }
     }
     if ((int)deg_lambda != count || deg_lambda == 0) { count = -1; goto finish; }   // 1577-1595
 
     nroot = (unsigned)count;
-    for (unsigned j = 0; j < nroot; ++j) wrote[j] = 0;
+    for (unsigned j = 0; j < nroot; ++j) wrote[(j) * kS] = 0;
     deg_omega = deg_lambda - 1;                                               // 1596-1604
     for (unsigned i = 0; i <= deg_omega; ++i) {
         unsigned tmp = 0;
         for (unsigned j = i + 1; j-- > 0;)
-            if (syn[i - j] != A0 && lambda[j] != A0) tmp ^= A[modnn(syn[i - j] + lambda[j], NN, mm)];
-        omega[i] = I[tmp];
+            if (syn[(i - j) * kS] != A0 && lambda[(j) * kS] != A0) tmp ^= A[modnn(syn[(i - j) * kS] + lambda[(j) * kS], NN, mm)];
+        omega[(i) * kS] = I[tmp];
     }
 
     for (unsigned j = (unsigned)count; j-- > 0;) {                           // Forney 1610-1690
-        const unsigned rj = root[j];
+        const unsigned rj = root[(j) * kS];
         unsigned num1 = 0;
         for (unsigned i = deg_omega + 1; i-- > 0;)
-            if (omega[i] != A0) num1 ^= A[modnn(omega[i] + i * rj, NN, mm)];
+            if (omega[(i) * kS] != A0) num1 ^= A[modnn(omega[(i) * kS] + i * rj, NN, mm)];
         const unsigned num2 = A[modnn(rj * (FCR - 1) + NN, NN, mm)];
         unsigned den = 0;
         const unsigned top = deg_lambda < NR - 1 ? deg_lambda : NR - 1;
         for (int i = (int)(top & ~1u); i >= 0; i -= 2)
-            if (lambda[i + 1] != A0) den ^= A[modnn(lambda[i + 1] + (unsigned)i * rj, NN, mm)];
+            if (lambda[(i + 1) * kS] != A0) den ^= A[modnn(lambda[(i + 1) * kS] + (unsigned)i * rj, NN, mm)];
         if (den == 0) { count = -1; goto finish; }
         if (num1 != 0) {
-            if (loc[j] < pad) { count = -1; goto finish; }
+            if (loc[(j) * kS] < pad) { count = -1; goto finish; }
             const unsigned cor = A[modnn(I[num1] + I[num2] + NN - I[den], NN, mm)];
             unsigned cv = cor;
             unsigned at, delta = cor;
-            if (loc[j] < NN - NR) {
-                at = loc[j] - pad;
+            if (loc[(j) * kS] < NN - NR) {
+                at = loc[(j) * kS] - pad;
                 if (c.dual) {
                     const unsigned err_dua = static_cast<unsigned>(data[at]) & NN;
                     delta = ID[FD[err_dua] ^ cor] ^ err_dua;
                     cv = delta;
                 }
             } else {
-                const unsigned pi = loc[j] - (NN - NR);
+                const unsigned pi = loc[(j) * kS] - (NN - NR);
                 at = len + pi;
                 if (c.dual) {
                     const unsigned err_dua = static_cast<unsigned>(parity[pi]);
@@ -255,10 +263,10 @@ __device__ int decode_one(const DevCodec &c, const uint16_t *__restrict__ A,
                     cv = cor;                                 // fix_cnv ^ err_cnv (1684)
                 }
             }
-            corrv[j] = (uint16_t)cv;
-            wrote[j] = 1;
-            fixp[nfix] = (uint16_t)at;
-            fixv[nfix] = (uint16_t)delta;
+            corrv[(j) * kS] = (uint16_t)cv;
+            wrote[(j) * kS] = 1;
+            fixp[(nfix) * kS] = (uint16_t)at;
+            fixv[(nfix) * kS] = (uint16_t)delta;
             ++nfix;
         }
     }
@@ -266,15 +274,15 @@ __device__ int decode_one(const DevCodec &c, const uint16_t *__restrict__ A,
 finish:
     if (!c.masked || count > 0)
         for (unsigned f = 0; f < nfix; ++f) {
-            const unsigned at = fixp[f];
-            if (at < len) data[at] = static_cast<T>(data[at] ^ fixv[f]);
-            else parity[at - len] = static_cast<T>(parity[at - len] ^ fixv[f]);
+            const unsigned at = fixp[(f) * kS];
+            if (at < len) data[at] = static_cast<T>(data[at] ^ fixv[(f) * kS]);
+            else parity[at - len] = static_cast<T>(parity[at - len] ^ fixv[(f) * kS]);
         }
     if (corr_out)  // corr is passed straight through by decode<INP> in both paths (1222, 1240)
         for (unsigned j = 0; j < nroot; ++j)
-            if (wrote[j]) corr_out[j] = static_cast<T>(corrv[j]);
+            if (wrote[(j) * kS]) corr_out[j] = static_cast<T>(corrv[(j) * kS]);
     if (pos_out && count > 0)
-        for (int i = 0; i < count; ++i) pos_out[i] = loc[i] - pad;
+        for (int i = 0; i < count; ++i) pos_out[i] = loc[(i) * kS] - pad;
     return count;
 }
 
@@ -301,9 +309,12 @@ constexpr int32_t kSentinel = INT32_MIN;
 // case -- costs a quarter of the blocks of a thread-per-codeword screen.
 constexpr int kFlagPer = 4;
 
-__global__ void __launch_bounds__(kBlock) k_decode_flagged(DevCodec c, DecodeArgs a,
-                                                           const uint8_t *syn_ws) {
+constexpr int kFlagBlock = 64;
+
+__global__ void __launch_bounds__(kFlagBlock) k_decode_flagged(DevCodec c, DecodeArgs a,
+                                                               const uint8_t *syn_ws) {
     __shared__ __attribute__((aligned(16))) uint16_t smem[2 * 256 + 256];
+    __shared__ uint8_t work[11 * 33 * kFlagBlock];
     const size_t k0 = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * kFlagPer;
     unsigned mine = 0;
     if (k0 + kFlagPer <= a.ncw && (reinterpret_cast<uintptr_t>(a.result + k0) & 15) == 0) {
@@ -328,8 +339,9 @@ __global__ void __launch_bounds__(kBlock) k_decode_flagged(DevCodec c, DecodeArg
         const unsigned ne = a.neras ? a.neras[k] : 0;
         uint32_t *pos = a.positions ? a.positions + k * a.pos_stride : nullptr;
         uint8_t *corr = a.corr ? static_cast<uint8_t *>(a.corr) + k * a.corr_stride : nullptr;
-        a.result[k] = decode_one<uint8_t, 32>(c, A, I, ID, FD, data, a.len, parity, eras, ne, pos,
-                                              corr, syn_ws + k * 32);
+        a.result[k] = decode_one<uint8_t, 32, kFlagBlock, uint8_t>(c, A, I, ID, FD, data, a.len, parity, eras,
+                                                          ne, pos, corr, syn_ws + k * 32,
+                                                          work + threadIdx.x);
     }
 }
 
@@ -362,9 +374,9 @@ hipError_t dec_launch(const DevCodec &c, const DecodeArgs &a, hipStream_t s) {
 hipError_t launch_decode_flagged(const DevCodec &c, const DecodeArgs &a, const uint8_t *syn_ws,
                                  hipStream_t s) {
     if (a.ncw == 0) return hipSuccess;
-    const size_t per = (size_t)kBlock * kFlagPer;
+    const size_t per = (size_t)kFlagBlock * kFlagPer;
     const unsigned grid = (unsigned)((a.ncw + per - 1) / per);
-    hipLaunchKernelGGL(k_decode_flagged, dim3(grid), dim3(kBlock), 0, s, c, a, syn_ws);
+    hipLaunchKernelGGL(k_decode_flagged, dim3(grid), dim3(kFlagBlock), 0, s, c, a, syn_ws);
     return hipGetLastError();
 }
 
