@@ -13,6 +13,7 @@ namespace ezrs {
 namespace {
 
 constexpr int kBlock = 256;
+constexpr int kDecBlock = 64;    // generic decode with NR <= 32: LDS working arrays per 64 lanes
 
 // x mod nn for x < 2^32 (Karn's fold, rs_base:648-657).
 __device__ __forceinline__ unsigned modnn(unsigned x, unsigned nn, unsigned mm) {
@@ -68,26 +69,30 @@ __global__ void __launch_bounds__(kBlock) k_encode_generic(DevCodec c, EncodeArg
     const unsigned NR = c.nroots, nn = c.nn, mm = c.mm;
 
     // Circular parity register: logical parity[j] lives at par[(head + j) % NR], so the
-    // reference's std::rotate (rs_base:1318) becomes a head increment.
-    uint16_t par[MAXR];
-    for (unsigned j = 0; j < NR; ++j) par[j] = 0;
+    // reference's std::rotate (rs_base:1318) becomes a head increment.  Its data-dependent index
+    // keeps it out of VGPRs: in LDS (lanes interleaved) for NR <= 32, private memory above.
+    constexpr int PS = MAXR <= 32 ? kBlock : 1;
+    __shared__ uint16_t pbuf[MAXR <= 32 ? MAXR * kBlock : 1];
+    uint16_t priv[MAXR <= 32 ? 1 : MAXR];
+    uint16_t *const par = MAXR <= 32 ? pbuf + threadIdx.x : priv;
+    for (unsigned j = 0; j < NR; ++j) par[(j) * PS] = 0;
     unsigned head = 0;
     for (unsigned i = 0; i < a.len; ++i) {
         unsigned sym = static_cast<unsigned>(data[i]) & nn;        // masked copy (rs_base:893)
         if (c.dual) sym = FD[sym];
-        const unsigned fb = I[sym ^ par[head]];
+        const unsigned fb = I[sym ^ par[(head) * PS]];
         if (fb != nn) {
             unsigned p = head + 1;
             for (unsigned j = 1; j < NR; ++j, ++p) {
                 if (p >= NR) p -= NR;
-                par[p] ^= A[modnn(fb + c.genpoly[NR - j], nn, mm)];
+                par[(p) * PS] ^= A[modnn(fb + c.genpoly[NR - j], nn, mm)];
             }
         }
-        par[head] = fb != nn ? A[modnn(fb + c.genpoly[0], nn, mm)] : 0;
+        par[(head) * PS] = fb != nn ? A[modnn(fb + c.genpoly[0], nn, mm)] : 0;
         if (++head == NR) head = 0;
     }
     for (unsigned j = 0, p = head; j < NR; ++j) {
-        unsigned v = par[p];
+        unsigned v = par[(p) * PS];
         parity[j] = static_cast<T>(c.dual ? ID[v] : v);
         if (++p == NR) p = 0;
     }
@@ -300,7 +305,13 @@ __global__ void __launch_bounds__(kBlock) k_decode_generic(DevCodec c, DecodeArg
     const unsigned ne = a.neras ? a.neras[k] : 0;
     uint32_t *pos = a.positions ? a.positions + k * a.pos_stride : nullptr;
     T *corr = a.corr ? static_cast<T *>(a.corr) + k * a.corr_stride : nullptr;
-    a.result[k] = decode_one<T, MAXR>(c, A, I, ID, FD, data, a.len, parity, eras, ne, pos, corr);
+    if constexpr (MAXR <= 32) {        // working arrays in LDS, lanes interleaved (kDecBlock lanes)
+        __shared__ uint16_t work[11 * (MAXR + 1) * kDecBlock];
+        a.result[k] = decode_one<T, MAXR, kDecBlock>(c, A, I, ID, FD, data, a.len, parity, eras, ne,
+                                                     pos, corr, nullptr, work + threadIdx.x);
+    } else {
+        a.result[k] = decode_one<T, MAXR>(c, A, I, ID, FD, data, a.len, parity, eras, ne, pos, corr);
+    }
 }
 
 constexpr int32_t kSentinel = INT32_MIN;
@@ -359,12 +370,13 @@ hipError_t enc_launch(const DevCodec &c, const EncodeArgs &a, hipStream_t s) {
 
 template <typename T, int MAXR>
 hipError_t dec_launch(const DevCodec &c, const DecodeArgs &a, hipStream_t s) {
-    const unsigned grid = (unsigned)((a.ncw + kBlock - 1) / kBlock);
+    const unsigned blk = MAXR <= 32 ? kDecBlock : kBlock;
+    const unsigned grid = (unsigned)((a.ncw + blk - 1) / blk);
     if (c.nn <= 4095) {
         const size_t sm = 2 * (c.nn + 1) * sizeof(uint16_t) + 512;
-        hipLaunchKernelGGL((k_decode_generic<T, MAXR, true>), dim3(grid), dim3(kBlock), sm, s, c, a);
+        hipLaunchKernelGGL((k_decode_generic<T, MAXR, true>), dim3(grid), dim3(blk), sm, s, c, a);
     } else {
-        hipLaunchKernelGGL((k_decode_generic<T, MAXR, false>), dim3(grid), dim3(kBlock), 0, s, c, a);
+        hipLaunchKernelGGL((k_decode_generic<T, MAXR, false>), dim3(grid), dim3(blk), 0, s, c, a);
     }
     return hipGetLastError();
 }
