@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "../../include/ezbch.h"
+#include "ezrs_internal.hpp"
 
 namespace {
 
@@ -736,11 +737,11 @@ int ezbch_encode_host(ezbch_codec *c, const uint8_t *data, size_t data_stride, u
     for (size_t k0 = 0; k0 < ncw; k0 += chunk) {
         const size_t n = ncw - k0 < chunk ? ncw - k0 : chunk;
         if (len)
-            HIP_TRY(hipMemcpy2DAsync(st, row, data + k0 * data_stride, data_stride, len, n,
+            HIP_TRY(ezrs::copy2d(st, row, data + k0 * data_stride, data_stride, len, n,
                                      hipMemcpyHostToDevice, c->stream));
         BchArgs a{st, row, len, st + len, row, nullptr, nullptr, 0, n, 0};
         HIP_TRY(launch_encode(c->dev, a, c->stream));
-        HIP_TRY(hipMemcpy2DAsync(ecc + k0 * ecc_stride, ecc_stride, st + len, row, eb, n,
+        HIP_TRY(ezrs::copy2d(ecc + k0 * ecc_stride, ecc_stride, st + len, row, eb, n,
                                  hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
     }
@@ -768,23 +769,23 @@ int ezbch_decode_host(ezbch_codec *c, uint8_t *data, size_t data_stride, unsigne
     for (size_t k0 = 0; k0 < ncw; k0 += chunk) {
         const size_t n = ncw - k0 < chunk ? ncw - k0 : chunk;
         if (len)
-            HIP_TRY(hipMemcpy2DAsync(st, row, data + k0 * data_stride, data_stride, len, n,
+            HIP_TRY(ezrs::copy2d(st, row, data + k0 * data_stride, data_stride, len, n,
                                      hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(hipMemcpy2DAsync(st + len, row, ecc + k0 * ecc_stride, ecc_stride, eb, n,
+        HIP_TRY(ezrs::copy2d(st + len, row, ecc + k0 * ecc_stride, ecc_stride, eb, n,
                                  hipMemcpyHostToDevice, c->stream));
         if (errloc)   // copy-in/copy-out: entries the decode does not write keep their value
-            HIP_TRY(hipMemcpy2DAsync(dloc, T * 4, errloc + k0 * errloc_stride, errloc_stride * 4,
+            HIP_TRY(ezrs::copy2d(dloc, T * 4, errloc + k0 * errloc_stride, errloc_stride * 4,
                                      T * 4, n, hipMemcpyHostToDevice, c->stream));
         BchArgs a{st, row, len, st + len, row, dres, errloc ? dloc : nullptr, T, n, 0};
         HIP_TRY(launch_decode(c->dev, a, c->stream));
         if (len)
-            HIP_TRY(hipMemcpy2DAsync(data + k0 * data_stride, data_stride, st, row, len, n,
+            HIP_TRY(ezrs::copy2d(data + k0 * data_stride, data_stride, st, row, len, n,
                                      hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipMemcpy2DAsync(ecc + k0 * ecc_stride, ecc_stride, st + len, row, eb, n,
+        HIP_TRY(ezrs::copy2d(ecc + k0 * ecc_stride, ecc_stride, st + len, row, eb, n,
                                  hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipMemcpyAsync(result + k0, dres, n * 4, hipMemcpyDeviceToHost, c->stream));
         if (errloc)
-            HIP_TRY(hipMemcpy2DAsync(errloc + k0 * errloc_stride, errloc_stride * 4, dloc, T * 4,
+            HIP_TRY(ezrs::copy2d(errloc + k0 * errloc_stride, errloc_stride * 4, dloc, T * 4,
                                      T * 4, n, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
     }

@@ -12,6 +12,15 @@
 
 namespace ezrs {
 
+// hipMemcpy2DAsync moves each row separately; when both pitches equal the row width the region
+// is contiguous and goes as one linear copy.
+inline hipError_t copy2d(void *dst, size_t dpitch, const void *src, size_t spitch, size_t width,
+                         size_t height, hipMemcpyKind kind, hipStream_t st) {
+    if (height == 1 || (dpitch == width && spitch == width))
+        return hipMemcpyAsync(dst, src, width * height, kind, st);
+    return hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, kind, st);
+}
+
 // Everything a kernel needs to know about a codec, passed by value at launch.
 struct DevCodec {
     unsigned mm, nn, nroots, load, fcr, prim, iprim, poly;

@@ -108,7 +108,10 @@ int ezrs_decode(const ezrs_codec *codec, void *data, size_t data_stride, unsigne
 
 /* Host-memory forms: the same contracts with HOST pointers.  The batch is streamed through the
  * device in chunks of `chunk` codewords (0 = library default) over two HIP streams with
- * asynchronous copies; pinned host memory (ezrs_host_alloc) gets full PCIe overlap.  Blocking:
+ * asynchronous copies; pinned host memory (ezrs_host_alloc) gets full PCIe overlap.  When the
+ * parity lies inside the row (parity == NULL, or data + len at the same stride), rows move as
+ * one linear copy per chunk each way, and ezrs_encode_host writes each row back whole (its data
+ * symbols unchanged).  Blocking:
  * they return when the results are back in host memory. */
 int ezrs_encode_host(ezrs_codec *codec, const void *data, size_t data_stride, unsigned len,
                      void *parity, size_t parity_stride, size_t ncw, size_t chunk);

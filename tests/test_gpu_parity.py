@@ -95,6 +95,38 @@ def test_golden_host_pipeline(torch, fn):
         np.testing.assert_array_equal(p[0], f["dec_parity_out"][t])
 
 
+@pytest.mark.parametrize("n,k,pad,pinned", [(255, 223, 0, False), (255, 223, 5, True),
+                                              (255, 251, 3, False), (1023, 991, 0, True)])
+def test_host_pipeline_inline_parity(torch, n, k, pad, pinned):
+    """Host forms with parity inside the row (the linear-copy path), several chunks, pageable and
+    pinned buffers: encode, then an 8-error/4-erasure (t=2 codecs: 1+1) decode, against the oracle."""
+    import ezrs
+    c = ezrs.Codec.rs(n, k)
+    oc = O.Codec(*O.rs_params(n, k))
+    nr = n - k
+    rng = np.random.default_rng(n * 7 + k + pad)
+    ncw, stride = 2500, n + pad
+    host = rng.integers(0, n + 1, (ncw, stride)).astype(c.dtype)
+    exp = host.copy()
+    oc.encode_batch(exp, k)
+    buf = torch.from_numpy(host.view(np.int16) if c.dtype == np.uint16 else host)
+    if pinned:
+        buf = buf.pin_memory()
+    h = buf.numpy().view(c.dtype)
+    c.encode_host(h, k, chunk=700)
+    np.testing.assert_array_equal(h, exp)                     # parity written, pad untouched
+    ne, nx = (8, 4) if nr >= 16 else (1, 1)
+    locs = np.argsort(rng.random((ncw, n)), axis=1)[:, :ne + nx]
+    rows = np.arange(ncw)[:, None]
+    h[rows, locs] ^= rng.integers(1, n + 1, (ncw, ne + nx)).astype(c.dtype)
+    eras = np.zeros((ncw, nr), np.uint32)
+    eras[:, :nx] = locs[:, ne:]
+    neras = np.full(ncw, nx, np.uint32)
+    r = c.decode_host(h, k, eras=eras, neras=neras, chunk=700)
+    assert (r == ne + nx).all()
+    np.testing.assert_array_equal(h, exp)
+
+
 def _inject(torch, cw, n_err, n_era, nn, gen):
     """Corrupt n_err + n_era distinct symbols per row; the last n_era are flagged as erasures."""
     ncw, n = cw.shape

@@ -15,7 +15,9 @@ run() {  # name timeout cmd...
 }
 run pytest 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
 run smoke 240 python -c "import __graft_entry__ as g; g.smoke()"
-run bench_c2 400 python bench.py --steps 20 --warmup 3
+run bench_c2 400 python bench.py --steps 20 --warmup 3 --e2e
+run bench_c3 400 python bench.py --workload c3 --steps 10 --warmup 2
+run bench_c4 400 python bench.py --workload c4 --steps 3 --warmup 1
 run bench_c5 400 python bench.py --workload c5 --steps 20 --warmup 3
 run prof_c2 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c2 -o run -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline
 run prof_c5 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c5 -o run -- python bench.py --workload c5 --steps 5 --warmup 1
