@@ -106,6 +106,13 @@ __global__ void __launch_bounds__(kBlock) k_encode_generic(DevCodec c, EncodeArg
 // with data-dependent indices would otherwise sit in waterfall-indexed VGPRs -- in LDS at `lds`,
 // element i of a lane's array at lds[i * WS] (lanes interleaved: conflict-free).  W is the element
 // type: uint16_t, or uint8_t where every value fits (m = 8: indices, log values and A0 = 255).
+// Working arrays per lane: arrays whose live ranges do not overlap share storage (root reuses b after
+// BM, omega reuses the Chien registers t, the Forney deltas reuse syn), the Forney "wrote" flags are
+// a register bitmask for MAXR <= 32, and fix positions are re-derived from loc.  Fewer bytes per lane
+// in LDS means more resident waves for the latency-bound flagged-codeword kernel.
+template <int MAXR>
+constexpr int kWorkArrays = MAXR <= 32 ? 6 : 7;
+
 template <typename T, int MAXR, int WS = 0, typename W = uint16_t>
 __device__ int decode_one(const DevCodec &c, const uint16_t *__restrict__ A,
                           const uint16_t *__restrict__ I, const uint8_t *ID, const uint8_t *FD,
@@ -125,13 +132,21 @@ __device__ int decode_one(const DevCodec &c, const uint16_t *__restrict__ A,
 
     constexpr int kS = WS ? WS : 1;
     constexpr int kW = MAXR + 1;       // elements per working array
-    W priv[WS ? 1 : 11 * kW];
+    W priv[WS ? 1 : kWorkArrays<MAXR> * kW];
     W *const base = WS ? lds : priv;
     W *syn = base, *lambda = base + kW * kS, *b = base + 2 * kW * kS, *t = base + 3 * kW * kS,
-             *omega = base + 4 * kW * kS, *root = base + 5 * kW * kS, *loc = base + 6 * kW * kS,
-             *fixv = base + 7 * kW * kS, *corrv = base + 8 * kW * kS, *fixp = base + 9 * kW * kS,
-             *wrote = base + 10 * kW * kS;   // wrote: corr[j] written by the reference's Forney loop
-    unsigned nfix = 0, nroot = 0;
+             *loc = base + 4 * kW * kS, *corrv = base + 5 * kW * kS;
+    W *const root = b, *const omega = t, *const fixv = syn;
+    // wrote[j]: corr[j] (and fix j) written by the reference's Forney loop
+    W *const wrote = kWorkArrays<MAXR> > 6 ? base + 6 * kW * kS : nullptr;
+    uint32_t wmask = 0;
+    auto set_wrote = [&](unsigned j) {
+        if constexpr (MAXR <= 32) wmask |= 1u << j; else wrote[j * kS] = 1;
+    };
+    auto has_wrote = [&](unsigned j) -> bool {
+        if constexpr (MAXR <= 32) return wmask >> j & 1; else return wrote[j * kS] != 0;
+    };
+    unsigned nroot = 0;
     int count = 0;
     unsigned deg_lambda = 0, deg_omega = 0, r = no_eras, el = no_eras;
 
@@ -226,7 +241,8 @@ __device__ int decode_one(const DevCodec &c, const uint16_t *__restrict__ A,
     if ((int)deg_lambda != count || deg_lambda == 0) { count = -1; goto finish; }   // 1577-1595
 
     nroot = (unsigned)count;
-    for (unsigned j = 0; j < nroot; ++j) wrote[(j) * kS] = 0;
+    if constexpr (MAXR > 32)
+        for (unsigned j = 0; j < nroot; ++j) wrote[(j) * kS] = 0;
     deg_omega = deg_lambda - 1;                                               // 1596-1604
     for (unsigned i = 0; i <= deg_omega; ++i) {
         unsigned tmp = 0;
@@ -268,24 +284,24 @@ __device__ int decode_one(const DevCodec &c, const uint16_t *__restrict__ A,
                     cv = cor;                                 // fix_cnv ^ err_cnv (1684)
                 }
             }
+            (void)at;
             corrv[(j) * kS] = (uint16_t)cv;
-            wrote[(j) * kS] = 1;
-            fixp[(nfix) * kS] = (uint16_t)at;
-            fixv[(nfix) * kS] = (uint16_t)delta;
-            ++nfix;
+            fixv[(j) * kS] = (uint16_t)delta;
+            set_wrote(j);
         }
     }
 
 finish:
-    if (!c.masked || count > 0)
-        for (unsigned f = 0; f < nfix; ++f) {
-            const unsigned at = fixp[(f) * kS];
-            if (at < len) data[at] = static_cast<T>(data[at] ^ fixv[(f) * kS]);
-            else parity[at - len] = static_cast<T>(parity[at - len] ^ fixv[(f) * kS]);
+    if (!c.masked || count > 0)   // roots are distinct, so the fixes commute
+        for (unsigned j = 0; j < nroot; ++j) {
+            if (!has_wrote(j)) continue;
+            const unsigned l = loc[(j) * kS];
+            if (l < NN - NR) data[l - pad] = static_cast<T>(data[l - pad] ^ fixv[(j) * kS]);
+            else parity[l - (NN - NR)] = static_cast<T>(parity[l - (NN - NR)] ^ fixv[(j) * kS]);
         }
     if (corr_out)  // corr is passed straight through by decode<INP> in both paths (1222, 1240)
         for (unsigned j = 0; j < nroot; ++j)
-            if (wrote[(j) * kS]) corr_out[j] = static_cast<T>(corrv[(j) * kS]);
+            if (has_wrote(j)) corr_out[j] = static_cast<T>(corrv[(j) * kS]);
     if (pos_out && count > 0)
         for (int i = 0; i < count; ++i) pos_out[i] = loc[(i) * kS] - pad;
     return count;
@@ -306,7 +322,7 @@ __global__ void __launch_bounds__(kBlock) k_decode_generic(DevCodec c, DecodeArg
     uint32_t *pos = a.positions ? a.positions + k * a.pos_stride : nullptr;
     T *corr = a.corr ? static_cast<T *>(a.corr) + k * a.corr_stride : nullptr;
     if constexpr (MAXR <= 32) {        // working arrays in LDS, lanes interleaved (kDecBlock lanes)
-        __shared__ uint16_t work[11 * (MAXR + 1) * kDecBlock];
+        __shared__ uint16_t work[kWorkArrays<MAXR> * (MAXR + 1) * kDecBlock];
         a.result[k] = decode_one<T, MAXR, kDecBlock>(c, A, I, ID, FD, data, a.len, parity, eras, ne,
                                                      pos, corr, nullptr, work + threadIdx.x);
     } else {
@@ -325,7 +341,7 @@ constexpr int kFlagBlock = 64;
 __global__ void __launch_bounds__(kFlagBlock) k_decode_flagged(DevCodec c, DecodeArgs a,
                                                                const uint8_t *syn_ws) {
     __shared__ __attribute__((aligned(16))) uint16_t smem[2 * 256 + 256];
-    __shared__ uint8_t work[11 * 33 * kFlagBlock];
+    __shared__ uint8_t work[kWorkArrays<32> * 33 * kFlagBlock];
     const size_t k0 = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * kFlagPer;
     unsigned mine = 0;
     if (k0 + kFlagPer <= a.ncw && (reinterpret_cast<uintptr_t>(a.result + k0) & 15) == 0) {
