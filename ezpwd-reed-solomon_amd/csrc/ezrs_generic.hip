@@ -111,7 +111,7 @@ __global__ void __launch_bounds__(kBlock) k_encode_generic(DevCodec c, EncodeArg
 // a register bitmask for MAXR <= 32, and fix positions are re-derived from loc.  Fewer bytes per lane
 // in LDS means more resident waves for the latency-bound flagged-codeword kernel.
 template <int MAXR>
-constexpr int kWorkArrays = MAXR <= 32 ? 6 : 7;
+constexpr int kWorkArrays = MAXR <= 32 ? 5 : 6;
 
 template <typename T, int MAXR, int WS = 0, typename W = uint16_t>
 __device__ int decode_one(const DevCodec &c, const uint16_t *__restrict__ A,
@@ -135,10 +135,14 @@ __device__ int decode_one(const DevCodec &c, const uint16_t *__restrict__ A,
     W priv[WS ? 1 : kWorkArrays<MAXR> * kW];
     W *const base = WS ? lds : priv;
     W *syn = base, *lambda = base + kW * kS, *b = base + 2 * kW * kS, *t = base + 3 * kW * kS,
-             *loc = base + 4 * kW * kS, *corrv = base + 5 * kW * kS;
+             *corrv = base + 4 * kW * kS;
     W *const root = b, *const omega = t, *const fixv = syn;
     // wrote[j]: corr[j] (and fix j) written by the reference's Forney loop
-    W *const wrote = kWorkArrays<MAXR> > 6 ? base + 6 * kW * kS : nullptr;
+    W *const wrote = kWorkArrays<MAXR> > 5 ? base + 5 * kW * kS : nullptr;
+    // loc[j]: the Chien loop's k for root i = root[j], k = i * iprim - 1 (mod NN) (1562-1575)
+    auto locof = [&](unsigned j) -> unsigned {
+        return (unsigned)(((uint64_t)root[(j) * kS] * c.iprim + NN - 1) % NN);
+    };
     uint32_t wmask = 0;
     auto set_wrote = [&](unsigned j) {
         if constexpr (MAXR <= 32) wmask |= 1u << j; else wrote[j * kS] = 1;
@@ -221,11 +225,30 @@ __device__ int decode_one(const DevCodec &c, const uint16_t *__restrict__ A,
         lambda[(i) * kS] = I[lambda[(i) * kS]];
         if (lambda[(i) * kS] != NN) deg_lambda = i;
     }
-    {                                                                         // Chien 1555-1584
+    if constexpr (MAXR <= 32) {                                               // Chien 1555-1584
+        // the Chien registers live in VGPRs: fully unrolled over j, so every index is a constant;
+        // terms above deg_lambda are skipped (wave-uniform in practice), as the reference's loop does
+        unsigned rg[MAXR + 1];
+#pragma unroll
+        for (int j = 1; j <= MAXR; ++j) rg[j] = j <= (int)deg_lambda ? lambda[(j) * kS] : A0;
+        count = 0;
+        for (unsigned i = 1; i <= NN; ++i) {
+            unsigned q = 1;
+#pragma unroll
+            for (int j = MAXR; j > 0; --j)
+                if (j <= (int)deg_lambda && rg[j] != A0) {
+                    rg[j] = modnn(rg[j] + j, NN, mm);
+                    q ^= A[rg[j]];
+                }
+            if (q != 0) continue;
+            root[(count) * kS] = (uint16_t)i;
+            if (++count == (int)deg_lambda) break;
+        }
+    } else {
         W *reg = t;
         for (unsigned i = 0; i <= NR; ++i) reg[(i) * kS] = lambda[(i) * kS];
         count = 0;
-        for (unsigned i = 1, k = c.iprim - 1; i <= NN; ++i, k = modnn(k + c.iprim, NN, mm)) {
+        for (unsigned i = 1; i <= NN; ++i) {
             unsigned q = 1;
             for (unsigned j = deg_lambda; j > 0; --j)
                 if (reg[(j) * kS] != A0) {
@@ -234,7 +257,6 @@ __device__ int decode_one(const DevCodec &c, const uint16_t *__restrict__ A,
                 }
             if (q != 0) continue;
             root[(count) * kS] = (uint16_t)i;
-            loc[(count) * kS] = (uint16_t)k;
             if (++count == (int)deg_lambda) break;
         }
     }
@@ -263,19 +285,19 @@ __device__ int decode_one(const DevCodec &c, const uint16_t *__restrict__ A,
             if (lambda[(i + 1) * kS] != A0) den ^= A[modnn(lambda[(i + 1) * kS] + (unsigned)i * rj, NN, mm)];
         if (den == 0) { count = -1; goto finish; }
         if (num1 != 0) {
-            if (loc[(j) * kS] < pad) { count = -1; goto finish; }
+            if (locof(j) < pad) { count = -1; goto finish; }
             const unsigned cor = A[modnn(I[num1] + I[num2] + NN - I[den], NN, mm)];
             unsigned cv = cor;
             unsigned at, delta = cor;
-            if (loc[(j) * kS] < NN - NR) {
-                at = loc[(j) * kS] - pad;
+            if (locof(j) < NN - NR) {
+                at = locof(j) - pad;
                 if (c.dual) {
                     const unsigned err_dua = static_cast<unsigned>(data[at]) & NN;
                     delta = ID[FD[err_dua] ^ cor] ^ err_dua;
                     cv = delta;
                 }
             } else {
-                const unsigned pi = loc[(j) * kS] - (NN - NR);
+                const unsigned pi = locof(j) - (NN - NR);
                 at = len + pi;
                 if (c.dual) {
                     const unsigned err_dua = static_cast<unsigned>(parity[pi]);
@@ -295,7 +317,7 @@ finish:
     if (!c.masked || count > 0)   // roots are distinct, so the fixes commute
         for (unsigned j = 0; j < nroot; ++j) {
             if (!has_wrote(j)) continue;
-            const unsigned l = loc[(j) * kS];
+            const unsigned l = locof(j);
             if (l < NN - NR) data[l - pad] = static_cast<T>(data[l - pad] ^ fixv[(j) * kS]);
             else parity[l - (NN - NR)] = static_cast<T>(parity[l - (NN - NR)] ^ fixv[(j) * kS]);
         }
@@ -303,7 +325,7 @@ finish:
         for (unsigned j = 0; j < nroot; ++j)
             if (has_wrote(j)) corr_out[j] = static_cast<T>(corrv[(j) * kS]);
     if (pos_out && count > 0)
-        for (int i = 0; i < count; ++i) pos_out[i] = loc[(i) * kS] - pad;
+        for (int i = 0; i < count; ++i) pos_out[i] = locof(i) - pad;
     return count;
 }
 
