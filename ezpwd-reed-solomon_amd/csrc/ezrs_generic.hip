@@ -233,13 +233,20 @@ __device__ int decode_one(const DevCodec &c, const uint16_t *__restrict__ A,
         for (int j = 1; j <= MAXR; ++j) rg[j] = j <= (int)deg_lambda ? lambda[(j) * kS] : A0;
         count = 0;
         for (unsigned i = 1; i <= NN; ++i) {
+            // blocks of 4 terms, branch-free inside (independent table loads can be in flight
+            // together): a zero coefficient stays A0 and adds alpha_to[A0] = 0; j <= deg < NN,
+            // so one conditional subtract reduces rg + j
             unsigned q = 1;
 #pragma unroll
-            for (int j = MAXR; j > 0; --j)
-                if (j <= (int)deg_lambda && rg[j] != A0) {
-                    rg[j] = modnn(rg[j] + j, NN, mm);
+            for (int j0 = 1; j0 <= MAXR; j0 += 4) {
+                if (j0 > (int)deg_lambda) break;
+#pragma unroll
+                for (int j = j0; j < j0 + 4 && j <= MAXR; ++j) {
+                    const unsigned x = rg[j] + j, y = x >= NN ? x - NN : x;
+                    rg[j] = rg[j] == A0 ? A0 : y;
                     q ^= A[rg[j]];
                 }
+            }
             if (q != 0) continue;
             root[(count) * kS] = (uint16_t)i;
             if (++count == (int)deg_lambda) break;
