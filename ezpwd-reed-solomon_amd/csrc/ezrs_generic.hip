@@ -195,19 +195,23 @@ __device__ int decode_one(const DevCodec &c, const uint16_t *__restrict__ A,
     for (unsigned i = 0; i <= NR; ++i) b[(i) * kS] = I[lambda[(i) * kS]];
 
     while (++r <= NR) {                                                       // BM 1507-1546
+        // branch-free terms: index_of[0] = A0, and a term with an A0 factor adds 0
         unsigned discr_r = 0;
-        for (unsigned i = 0; i < r; ++i)
-            if (lambda[(i) * kS] != 0 && syn[(r - i - 1) * kS] != A0)
-                discr_r ^= A[modnn(I[lambda[(i) * kS]] + syn[(r - i - 1) * kS], NN, mm)];
+        for (unsigned i = 0; i < r; ++i) {
+            const unsigned li = I[lambda[(i) * kS]], si = syn[(r - i - 1) * kS];
+            const unsigned x = li + si, y = x >= NN ? x - NN : x;
+            discr_r ^= (li == A0 || si == A0) ? 0u : (unsigned)A[y];
+        }
         discr_r = I[discr_r];
         if (discr_r == A0) {
             for (unsigned i = NR; i > 0; --i) b[(i) * kS] = b[(i - 1) * kS];
             b[(0) * kS] = (uint16_t)A0;
         } else {
             t[(0) * kS] = lambda[(0) * kS];
-            for (unsigned i = 0; i < NR; ++i)
-                t[(i + 1) * kS] = b[(i) * kS] != A0 ? (uint16_t)(lambda[(i + 1) * kS] ^ A[modnn(discr_r + b[(i) * kS], NN, mm)])
-                                      : lambda[(i + 1) * kS];
+            for (unsigned i = 0; i < NR; ++i) {
+                const unsigned bi = b[(i) * kS], x = discr_r + bi, y = x >= NN ? x - NN : x;
+                t[(i + 1) * kS] = (W)(lambda[(i + 1) * kS] ^ (bi == A0 ? 0u : (unsigned)A[y]));
+            }
             if (2 * el <= r + no_eras - 1) {
                 el = r + no_eras - el;
                 for (unsigned i = 0; i <= NR; ++i)
