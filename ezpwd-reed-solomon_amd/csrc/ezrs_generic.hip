@@ -99,6 +99,62 @@ __global__ void __launch_bounds__(kBlock) k_encode_generic(DevCodec c, EncodeArg
 }
 
 // ------------------------------------------------------------------------------------------------
+// encode_symbols with a 32-lane group per codeword (NR <= 32): lane j holds logical parity[j] of
+// the reference's rotating register (rs_base:1296-1332).  One data symbol per step:
+//   fb = index_of[sym ^ parity[0]];  parity'[j] = parity[j+1] ^ alpha_to[fb + genpoly[NR-1-j]]
+// (parity[NR] = 0; nothing is added when fb = A0), i.e. the reference's XOR-then-rotate with the
+// rotation done by a lane shift.  For long codewords (m > 8: up to 65535 symbols) the per-step
+// latency is spread over 32x fewer codewords per lane, and 32x more lanes are busy.
+constexpr int kLaneGroup = 32;
+
+template <typename T, bool LDS>
+__global__ void __launch_bounds__(kBlock) k_encode_lanes(DevCodec c, EncodeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+    const uint16_t *A, *I;
+    const uint8_t *ID, *FD;
+    stage_tables<LDS>(c, smem, A, I, ID, FD);
+    const unsigned j = threadIdx.x & (kLaneGroup - 1);
+    const size_t k = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / kLaneGroup;
+    if (k >= a.ncw) return;                 // uniform over the group
+    const T *data = static_cast<const T *>(a.data) + k * a.data_stride;
+    T *parity = static_cast<T *>(a.parity) + k * a.parity_stride;
+    const unsigned NR = c.nroots, nn = c.nn;
+    const unsigned g = j < NR ? c.genpoly[NR - 1 - j] : 0;
+    unsigned par = 0;
+    for (unsigned i0 = 0; i0 < a.len; i0 += kLaneGroup) {
+        unsigned dv = 0;
+        if (i0 + j < a.len) {
+            dv = static_cast<unsigned>(data[i0 + j]) & nn;            // masked copy (rs_base:893)
+            if (c.dual) dv = FD[dv];
+        }
+        const unsigned cnt = a.len - i0 < (unsigned)kLaneGroup ? a.len - i0 : kLaneGroup;
+        for (unsigned s = 0; s < cnt; ++s) {
+            const unsigned sym = __shfl(dv, (int)s, kLaneGroup);
+            const unsigned p0 = __shfl(par, 0, kLaneGroup);
+            unsigned nxt = __shfl_down(par, 1, kLaneGroup);
+            nxt = j + 1 < NR ? nxt : 0u;
+            const unsigned fb = I[sym ^ p0];
+            const unsigned x = fb + g, y = x >= nn ? x - nn : x;
+            par = j < NR ? (nxt ^ (fb != nn ? (unsigned)A[y] : 0u)) : 0u;
+        }
+    }
+    if (j < NR) parity[j] = static_cast<T>(c.dual ? ID[par] : par);
+}
+
+template <typename T>
+hipError_t enc_lanes_launch(const DevCodec &c, const EncodeArgs &a, hipStream_t s) {
+    const size_t threads = a.ncw * kLaneGroup;
+    const unsigned grid = (unsigned)((threads + kBlock - 1) / kBlock);
+    if (c.nn <= 4095) {
+        const size_t sm = 2 * (c.nn + 1) * sizeof(uint16_t) + 512;
+        hipLaunchKernelGGL((k_encode_lanes<T, true>), dim3(grid), dim3(kBlock), sm, s, c, a);
+    } else {
+        hipLaunchKernelGGL((k_encode_lanes<T, false>), dim3(grid), dim3(kBlock), 0, s, c, a);
+    }
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
 // decode_symbols on one codeword.  Corrections are recorded and applied at the end: for the direct
 // path every recorded correction (the reference corrects in place, so partial corrections before a
 // failure persist, rs_base:1238-1241), for the masked path only when count > 0 (rs_base:1223-1234).
@@ -444,7 +500,8 @@ hipError_t launch_decode_flagged(const DevCodec &c, const DecodeArgs &a, const u
 hipError_t launch_encode_generic(const DevCodec &c, const EncodeArgs &a, hipStream_t s) {
     if (a.ncw == 0) return hipSuccess;
     if (c.mm <= 8) return c.nroots <= 32 ? enc_launch<uint8_t, 32>(c, a, s) : enc_launch<uint8_t, 256>(c, a, s);
-    return c.nroots <= 32 ? enc_launch<uint16_t, 32>(c, a, s) : enc_launch<uint16_t, 256>(c, a, s);
+    // wide symbols (long codewords): a lane group per codeword
+    return c.nroots <= 32 ? enc_lanes_launch<uint16_t>(c, a, s) : enc_launch<uint16_t, 256>(c, a, s);
 }
 
 hipError_t launch_decode_generic(const DevCodec &c, const DecodeArgs &a, hipStream_t s) {
