@@ -169,12 +169,12 @@ hipError_t enc_lanes_launch(const DevCodec &c, const EncodeArgs &a, hipStream_t 
 template <int MAXR>
 constexpr int kWorkArrays = MAXR <= 32 ? 5 : 6;
 
-template <typename T, int MAXR, int WS = 0, typename W = uint16_t>
+template <typename T, int MAXR, int WS = 0, typename W = uint16_t, typename SY = uint8_t>
 __device__ int decode_one(const DevCodec &c, const uint16_t *__restrict__ A,
                           const uint16_t *__restrict__ I, const uint8_t *ID, const uint8_t *FD,
                           T *data, unsigned len, T *parity, const uint32_t *eras,
                           unsigned no_eras, uint32_t *pos_out, T *corr_out,
-                          const uint8_t *syn_in = nullptr, W *lds = nullptr) {
+                          const SY *syn_in = nullptr, W *lds = nullptr) {
     const unsigned NR = c.nroots, NN = c.nn, A0 = c.nn, mm = c.mm, LOAD = c.load;
     const unsigned FCR = c.fcr, PRM = c.prim;
     if (len == 0 || len > LOAD) return -1;                                    // 1375-1377
@@ -396,6 +396,69 @@ finish:
     return count;
 }
 
+// Wide symbols, NR <= 32: a 32-lane group per codeword evaluates the syndromes (lane i: S_i by
+// Horner over data then parity, rs_base:1390-1414, one symbol per step broadcast across the
+// group); lane 0 then runs the reference decode on them with its working arrays in LDS.
+template <typename T, bool LDS>
+__global__ void __launch_bounds__(kBlock) k_decode_lanes(DevCodec c, DecodeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+    constexpr int kGroups = kBlock / kLaneGroup;
+    __shared__ uint16_t sy[kGroups * kLaneGroup];
+    __shared__ uint16_t work[kGroups * kWorkArrays<32> * 33];
+    const uint16_t *A, *I;
+    const uint8_t *ID, *FD;
+    stage_tables<LDS>(c, smem, A, I, ID, FD);
+    const unsigned j = threadIdx.x & (kLaneGroup - 1), grp = threadIdx.x / kLaneGroup;
+    const size_t k = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / kLaneGroup;
+    const bool valid = k < a.ncw;                       // uniform over the group
+    const unsigned NR = c.nroots, NN = c.nn, len = a.len;
+    T *data = nullptr, *parity = nullptr;
+    if (valid) {
+        data = static_cast<T *>(a.data) + k * a.data_stride;
+        parity = static_cast<T *>(a.parity) + k * a.parity_stride;
+        const unsigned root = (unsigned)(((uint64_t)(c.fcr + j) * c.prim) % NN);
+        const unsigned tot = len + NR;
+        unsigned sv = 0;
+        for (unsigned i0 = 0; i0 < tot; i0 += kLaneGroup) {
+            unsigned dv = 0;
+            const unsigned at = i0 + j;
+            if (at < tot) {
+                dv = static_cast<unsigned>(at < len ? data[at] : parity[at - len]) & NN;
+                if (c.dual) dv = FD[dv];
+            }
+            const unsigned cnt = tot - i0 < (unsigned)kLaneGroup ? tot - i0 : kLaneGroup;
+            for (unsigned t = 0; t < cnt; ++t) {
+                const unsigned x = __shfl(dv, (int)t, kLaneGroup);
+                const unsigned li = I[sv], e = li + root, y = e >= NN ? e - NN : e;
+                sv = sv == 0 ? x : x ^ (unsigned)A[y];
+            }
+        }
+        sy[grp * kLaneGroup + j] = (uint16_t)sv;
+    }
+    __syncthreads();
+    if (!valid || j != 0) return;
+    const uint32_t *eras = a.eras ? a.eras + k * a.eras_stride : nullptr;
+    const unsigned ne = a.neras ? a.neras[k] : 0;
+    uint32_t *pos = a.positions ? a.positions + k * a.pos_stride : nullptr;
+    T *corr = a.corr ? static_cast<T *>(a.corr) + k * a.corr_stride : nullptr;
+    a.result[k] = decode_one<T, 32, 1, uint16_t, uint16_t>(c, A, I, ID, FD, data, len, parity, eras,
+                                                          ne, pos, corr, sy + grp * kLaneGroup,
+                                                          work + grp * kWorkArrays<32> * 33);
+}
+
+template <typename T>
+hipError_t dec_lanes_launch(const DevCodec &c, const DecodeArgs &a, hipStream_t s) {
+    const size_t threads = a.ncw * kLaneGroup;
+    const unsigned grid = (unsigned)((threads + kBlock - 1) / kBlock);
+    if (c.nn <= 4095) {
+        const size_t sm = 2 * (c.nn + 1) * sizeof(uint16_t) + 512;
+        hipLaunchKernelGGL((k_decode_lanes<T, true>), dim3(grid), dim3(kBlock), sm, s, c, a);
+    } else {
+        hipLaunchKernelGGL((k_decode_lanes<T, false>), dim3(grid), dim3(kBlock), 0, s, c, a);
+    }
+    return hipGetLastError();
+}
+
 template <typename T, int MAXR, bool LDS>
 __global__ void __launch_bounds__(kBlock) k_decode_generic(DevCodec c, DecodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
@@ -413,7 +476,7 @@ __global__ void __launch_bounds__(kBlock) k_decode_generic(DevCodec c, DecodeArg
     if constexpr (MAXR <= 32) {        // working arrays in LDS, lanes interleaved (kDecBlock lanes)
         __shared__ uint16_t work[kWorkArrays<MAXR> * (MAXR + 1) * kDecBlock];
         a.result[k] = decode_one<T, MAXR, kDecBlock>(c, A, I, ID, FD, data, a.len, parity, eras, ne,
-                                                     pos, corr, nullptr, work + threadIdx.x);
+                                                     pos, corr, static_cast<const uint8_t *>(nullptr), work + threadIdx.x);
     } else {
         a.result[k] = decode_one<T, MAXR>(c, A, I, ID, FD, data, a.len, parity, eras, ne, pos, corr);
     }
@@ -507,7 +570,8 @@ hipError_t launch_encode_generic(const DevCodec &c, const EncodeArgs &a, hipStre
 hipError_t launch_decode_generic(const DevCodec &c, const DecodeArgs &a, hipStream_t s) {
     if (a.ncw == 0) return hipSuccess;
     if (c.mm <= 8) return c.nroots <= 32 ? dec_launch<uint8_t, 32>(c, a, s) : dec_launch<uint8_t, 256>(c, a, s);
-    return c.nroots <= 32 ? dec_launch<uint16_t, 32>(c, a, s) : dec_launch<uint16_t, 256>(c, a, s);
+    // wide symbols (long codewords): syndromes by a lane group per codeword
+    return c.nroots <= 32 ? dec_lanes_launch<uint16_t>(c, a, s) : dec_launch<uint16_t, 256>(c, a, s);
 }
 
 } // namespace ezrs
