@@ -127,6 +127,47 @@ def test_host_pipeline_inline_parity(torch, n, k, pad, pinned):
     np.testing.assert_array_equal(h, exp)
 
 
+@pytest.mark.parametrize("n,k,ncw,L", [(65535, 65503, 6, 65503), (65535, 65503, 40, 900),
+                                        (1023, 1001, 300, 1001), (4095, 4063, 50, 2000)])
+def test_wide_symbol_lane_kernels_vs_oracle(torch, n, k, ncw, L):
+    """m > 8, NR <= 32: the lane-group encode and syndrome/decode kernels against the oracle --
+    parity, result, positions and corrected rows -- with 8 errors + 4 erasures per row."""
+    import ezrs
+    c = ezrs.Codec.rs(n, k)
+    oc = O.Codec(*O.rs_params(n, k))
+    nr = n - k
+    rng = np.random.default_rng(n + ncw)
+    host = rng.integers(0, n + 1, (ncw, L + nr)).astype(np.uint16)
+    ref = host.copy()
+    oc.encode_batch(ref, L)
+    dev = _to_dev(torch, host)
+    c.encode(dev, L)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_to_np(dev, np.uint16), ref)
+    bad = ref.copy()
+    locs = np.stack([rng.choice(L + nr, 12, replace=False) for _ in range(ncw)])
+    rows = np.arange(ncw)[:, None]
+    bad[rows, locs] ^= rng.integers(1, n + 1, (ncw, 12)).astype(np.uint16)
+    eras = np.zeros((ncw, nr), np.uint32)
+    eras[:, :4] = locs[:, 8:]
+    neras = np.full(ncw, 4, np.uint32)
+    exp = bad.copy()
+    exp_pos = np.zeros((ncw, nr), np.uint32)
+    exp_r = oc.decode_batch(exp, L, None, eras, neras, exp_pos)
+    d = _to_dev(torch, bad)
+    pos = torch.zeros((ncw, nr), dtype=torch.int32, device="cuda")
+    r = c.decode(d, L, eras=torch.from_numpy(eras.view(np.int32)).cuda(),
+                 neras=torch.from_numpy(neras.view(np.int32)).cuda(), positions=pos)
+    torch.cuda.synchronize()
+    r = r.cpu().numpy()
+    np.testing.assert_array_equal(r, exp_r)
+    np.testing.assert_array_equal(_to_np(d, np.uint16), exp)
+    got_pos = pos.cpu().numpy().view(np.uint32)
+    for i in range(ncw):
+        if r[i] > 0:
+            np.testing.assert_array_equal(got_pos[i, :r[i]], exp_pos[i, :r[i]])
+
+
 def _inject(torch, cw, n_err, n_era, nn, gen):
     """Corrupt n_err + n_era distinct symbols per row; the last n_era are flagged as erasures."""
     ncw, n = cw.shape
