@@ -110,8 +110,8 @@ def load_traffic(kernel_call):
 
 def bench_rs_errors(args):
     """C3: RS(255,223), 1M codewords, each with 12 corrupted symbols of which the last 4 are passed as
-    erasures (exercise.H:174-177); C4: RS(65535,65503), 4096 codewords (--ncw; 65536 is the full
-    config), same corruption.  One step = encode the clean batch + decode a corrupted copy (restored
+    erasures (exercise.H:174-177); C4: RS(65535,65503), 65536 codewords (the full config; --ncw for
+    fewer), same corruption.  One step = encode the clean batch + decode a corrupted copy (restored
     from a master before each decode, outside the timed kernels).  value = codeword bytes encoded
     and decoded per second of kernel time (HIP events), summed over ranks."""
     import numpy as np
@@ -127,7 +127,7 @@ def bench_rs_errors(args):
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     c3 = args.workload == "c3"
     n, k = (255, 223) if c3 else (65535, 65503)
-    ncw = args.ncw if (c3 or args.ncw != 1 << 20) else 4096
+    ncw = args.ncw if (c3 or args.ncw != 1 << 20) else 65536     # C4: 64k codewords (configs[3])
     c = ezrs.Codec.rs(n, k, device=local)
     c.reserve(ncw)
     w = 1 if c3 else 2
