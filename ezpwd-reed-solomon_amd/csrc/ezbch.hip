@@ -734,6 +734,25 @@ int ezbch_encode_host(ezbch_codec *c, const uint8_t *data, size_t data_stride, u
     if (chunk > ncw) chunk = ncw;
     if (int r = ensure_stage(c, align_up(chunk * row))) return r;
     uint8_t *st = static_cast<uint8_t *>(c->d_stage);
+    // ECC inside the row: rows move as one linear copy each way (a 2-D copy of eb-byte pieces at
+    // row pitch runs row by row); the data bytes written back are the ones just read, unchanged.
+    const bool inline_ecc = ncw > 1 && ecc == data + len && ecc_stride == data_stride &&
+                            data_stride >= row;
+    if (inline_ecc) {
+        if (int r = ensure_stage(c, align_up(chunk * data_stride))) return r;
+        st = static_cast<uint8_t *>(c->d_stage);
+        for (size_t k0 = 0; k0 < ncw; k0 += chunk) {
+            const size_t n = ncw - k0 < chunk ? ncw - k0 : chunk;
+            const size_t span = (n - 1) * data_stride + row;
+            uint8_t *h = const_cast<uint8_t *>(data) + k0 * data_stride;
+            HIP_TRY(hipMemcpyAsync(st, h, span, hipMemcpyHostToDevice, c->stream));
+            BchArgs a{st, data_stride, len, st + len, data_stride, nullptr, nullptr, 0, n, 0};
+            HIP_TRY(launch_encode(c->dev, a, c->stream));
+            HIP_TRY(hipMemcpyAsync(h, st, span, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipStreamSynchronize(c->stream));
+        }
+        return 0;
+    }
     for (size_t k0 = 0; k0 < ncw; k0 += chunk) {
         const size_t n = ncw - k0 < chunk ? ncw - k0 : chunk;
         if (len)
