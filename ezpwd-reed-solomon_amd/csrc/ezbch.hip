@@ -50,7 +50,8 @@ struct DevBch {
 };
 
 struct BchArgs {
-    uint8_t *data;
+    const uint8_t *data;      // rows read by both kernels
+    uint8_t *wdata;           // the same rows, written by decode (corrections); null for encode
     size_t dstride;
     unsigned len;
     uint8_t *ecc;
@@ -414,7 +415,7 @@ __global__ void __launch_bounds__(kThreads) k_bch_decode(DevBch b, BchArgs a) {
         a.result[k] = -kEINVAL;
         return;
     }
-    uint8_t *d = a.data + k * a.dstride, *e = a.ecc + k * a.estride;
+    uint8_t *d = a.wdata + k * a.dstride, *e = a.ecc + k * a.estride;
     uint64_t r = data_remainder(reinterpret_cast<const uint64_t *>(smem), row, a.len);
     for (int i = 0; i < b.ecc_bytes; ++i) r ^= (uint64_t)e[i] << (56 - 8 * i);
     if (!r) {
@@ -565,6 +566,8 @@ struct ezbch_codec {
     std::mutex mu;                // guards the host-pipeline buffers
     void *d_stage = nullptr;
     size_t stage_bytes = 0;
+    void *h_stage = nullptr;      // pinned host staging (gathers, compact ECC)
+    size_t hstage_bytes = 0;
     hipStream_t stream = nullptr;
 };
 
@@ -626,17 +629,27 @@ int create_impl(ezbch_codec **out, unsigned m, unsigned t, unsigned poly, int de
     return 0;
 }
 
-int check_rows(const ezbch_codec *c, const uint8_t *data, size_t dstride, unsigned len,
-               uint8_t *&ecc, size_t &estride, size_t ncw) {
-    if (!data) return -EINVAL;
-    if (!ecc) {
-        ecc = const_cast<uint8_t *>(data) + len;
-        estride = dstride;
-        if (ncw > 1 && dstride < (size_t)len + c->h.ecc_bytes) return -EINVAL;
-    } else if (ncw > 1 && estride < c->h.ecc_bytes) {
-        return -EINVAL;
-    }
-    if (ncw > 1 && dstride < len) return -EINVAL;
+int check_args(const ezbch_codec *c, const uint8_t *data, size_t dstride, unsigned len,
+               const uint8_t *ecc, size_t estride, size_t ncw) {
+    if (!data || !ecc) return -EINVAL;
+    if (ncw > 1 && (estride < c->h.ecc_bytes || dstride < len)) return -EINVAL;
+    return 0;
+}
+
+// Row form: the ECC follows the data in each row.
+int check_rows(const ezbch_codec *c, const uint8_t *rows, size_t stride, unsigned len, size_t ncw) {
+    if (!rows) return -EINVAL;
+    if (ncw > 1 && stride < (size_t)len + c->h.ecc_bytes) return -EINVAL;
+    return 0;
+}
+
+int ensure_hstage(ezbch_codec *c, size_t bytes) {
+    if (c->hstage_bytes >= bytes) return 0;
+    if (c->h_stage) (void)hipHostFree(c->h_stage);
+    c->h_stage = nullptr;
+    c->hstage_bytes = 0;
+    HIP_TRY(hipHostMalloc(&c->h_stage, bytes, hipHostMallocDefault));
+    c->hstage_bytes = bytes;
     return 0;
 }
 
@@ -680,6 +693,7 @@ int ezbch_destroy(ezbch_codec *c) {
     if (c->d_step) (void)hipFree(c->d_step);
     if (c->d_tabs) (void)hipFree(c->d_tabs);
     if (c->d_stage) (void)hipFree(c->d_stage);
+    if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return 0;
@@ -701,11 +715,19 @@ int ezbch_encode(const ezbch_codec *c, const uint8_t *data, size_t data_stride, 
                  uint8_t *ecc, size_t ecc_stride, size_t ncw, void *stream) {
     if (!c) return -EINVAL;
     if (ncw == 0) return 0;
-    if (int r = check_rows(c, data, data_stride, len, ecc, ecc_stride, ncw)) return r;
+    if (int r = check_args(c, data, data_stride, len, ecc, ecc_stride, ncw)) return r;
     DeviceGuard g(c->device);
-    BchArgs a{const_cast<uint8_t *>(data), data_stride, len, ecc, ecc_stride, nullptr, nullptr, 0, ncw, 0};
+    BchArgs a{data, nullptr, data_stride, len, ecc, ecc_stride, nullptr, nullptr, 0, ncw, 0};
     hipError_t e = launch_encode(c->dev, a, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? 0 : hip_fail(e, "BCH encode launch");
+}
+
+int ezbch_encode_rows(const ezbch_codec *c, uint8_t *rows, size_t stride, unsigned len,
+                      size_t ncw, void *stream) {
+    if (!c) return -EINVAL;
+    if (ncw == 0) return 0;
+    if (int r = check_rows(c, rows, stride, len, ncw)) return r;
+    return ezbch_encode(c, rows, stride, len, rows + len, stride, ncw, stream);
 }
 
 int ezbch_decode(const ezbch_codec *c, uint8_t *data, size_t data_stride, unsigned len,
@@ -714,57 +736,80 @@ int ezbch_decode(const ezbch_codec *c, uint8_t *data, size_t data_stride, unsign
     if (!c) return -EINVAL;
     if (ncw == 0) return 0;
     if (!result) return -EINVAL;
-    if (int r = check_rows(c, data, data_stride, len, ecc, ecc_stride, ncw)) return r;
+    if (!ecc) {   // ECC inside the row
+        if (int r = check_rows(c, data, data_stride, len, ncw)) return r;
+        ecc = data + len;
+        ecc_stride = data_stride;
+    }
+    if (int r = check_args(c, data, data_stride, len, ecc, ecc_stride, ncw)) return r;
     if (errloc && ncw > 1 && errloc_stride < c->h.t) return -EINVAL;
     DeviceGuard g(c->device);
-    BchArgs a{data, data_stride, len, ecc, ecc_stride, result, errloc, errloc_stride, ncw, 0};
+    BchArgs a{data, data, data_stride, len, ecc, ecc_stride, result, errloc, errloc_stride, ncw, 0};
     hipError_t e = launch_decode(c->dev, a, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? 0 : hip_fail(e, "BCH decode launch");
 }
+
+namespace {
+
+// Host encode: rows' data bytes go to the device (one linear copy of the span when the pitch is at
+// most twice the row, else a CPU gather into pinned staging), the kernel writes a compact
+// [n][ecc_bytes] block, only that block comes back and a CPU scatter places each row's ECC.  The
+// caller's data bytes are never written.
+int bch_encode_host_core(ezbch_codec *c, const uint8_t *data, size_t data_stride, unsigned len,
+                         uint8_t *ecc, size_t ecc_stride, size_t ncw, size_t chunk) {
+    const size_t eb = c->h.ecc_bytes;
+    const bool span = ncw == 1 || data_stride <= 2 * (size_t)len + eb;
+    const size_t drow = span ? data_stride : len;
+    const bool ecc_direct = ecc_stride == eb || ncw == 1;
+    if (!chunk) chunk = ((size_t)64 << 20) / (drow ? drow : 1) + 1;
+    if (chunk > ncw) chunk = ncw;
+    const size_t b_in = align_up(chunk * drow + 16), b_ecc = align_up(chunk * eb);
+    if (int r = ensure_stage(c, b_in + b_ecc)) return r;
+    if (int r = ensure_hstage(c, (span ? 0 : align_up(chunk * len)) + (ecc_direct ? 0 : b_ecc) + 256))
+        return r;
+    uint8_t *st = static_cast<uint8_t *>(c->d_stage), *dec = st + b_in;
+    uint8_t *hs = static_cast<uint8_t *>(c->h_stage);
+    uint8_t *hin = hs, *hecc = hs + (span ? 0 : align_up(chunk * len));
+    for (size_t k0 = 0; k0 < ncw; k0 += chunk) {
+        const size_t n = ncw - k0 < chunk ? ncw - k0 : chunk;
+        const uint8_t *hd = data + k0 * data_stride;
+        if (span) {
+            HIP_TRY(hipMemcpyAsync(st, hd, (n - 1) * data_stride + len, hipMemcpyHostToDevice, c->stream));
+        } else {
+            for (size_t r = 0; r < n; ++r) std::memcpy(hin + r * len, hd + r * data_stride, len);
+            HIP_TRY(hipMemcpyAsync(st, hin, n * len, hipMemcpyHostToDevice, c->stream));
+        }
+        BchArgs a{st, nullptr, drow, len, dec, eb, nullptr, nullptr, 0, n, 0};
+        HIP_TRY(launch_encode(c->dev, a, c->stream));
+        HIP_TRY(hipMemcpyAsync(ecc_direct ? ecc + k0 * eb : hecc, dec, n * eb, hipMemcpyDeviceToHost,
+                               c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (!ecc_direct)
+            for (size_t r = 0; r < n; ++r) std::memcpy(ecc + (k0 + r) * ecc_stride, hecc + r * eb, eb);
+    }
+    return 0;
+}
+
+} // namespace
 
 int ezbch_encode_host(ezbch_codec *c, const uint8_t *data, size_t data_stride, unsigned len,
                       uint8_t *ecc, size_t ecc_stride, size_t ncw, size_t chunk) {
     if (!c) return -EINVAL;
     if (ncw == 0) return 0;
-    if (int r = check_rows(c, data, data_stride, len, ecc, ecc_stride, ncw)) return r;
+    if (int r = check_args(c, data, data_stride, len, ecc, ecc_stride, ncw)) return r;
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard g(c->device);
-    const size_t eb = c->h.ecc_bytes, row = (size_t)len + eb;
-    if (!chunk) chunk = ((size_t)64 << 20) / row + 1;
-    if (chunk > ncw) chunk = ncw;
-    if (int r = ensure_stage(c, align_up(chunk * row))) return r;
-    uint8_t *st = static_cast<uint8_t *>(c->d_stage);
-    // ECC inside the row: rows move as one linear copy each way (a 2-D copy of eb-byte pieces at
-    // row pitch runs row by row); the data bytes written back are the ones just read, unchanged.
-    const bool inline_ecc = ncw > 1 && ecc == data + len && ecc_stride == data_stride &&
-                            data_stride >= row;
-    if (inline_ecc) {
-        if (int r = ensure_stage(c, align_up(chunk * data_stride))) return r;
-        st = static_cast<uint8_t *>(c->d_stage);
-        for (size_t k0 = 0; k0 < ncw; k0 += chunk) {
-            const size_t n = ncw - k0 < chunk ? ncw - k0 : chunk;
-            const size_t span = (n - 1) * data_stride + row;
-            uint8_t *h = const_cast<uint8_t *>(data) + k0 * data_stride;
-            HIP_TRY(hipMemcpyAsync(st, h, span, hipMemcpyHostToDevice, c->stream));
-            BchArgs a{st, data_stride, len, st + len, data_stride, nullptr, nullptr, 0, n, 0};
-            HIP_TRY(launch_encode(c->dev, a, c->stream));
-            HIP_TRY(hipMemcpyAsync(h, st, span, hipMemcpyDeviceToHost, c->stream));
-            HIP_TRY(hipStreamSynchronize(c->stream));
-        }
-        return 0;
-    }
-    for (size_t k0 = 0; k0 < ncw; k0 += chunk) {
-        const size_t n = ncw - k0 < chunk ? ncw - k0 : chunk;
-        if (len)
-            HIP_TRY(ezrs::copy2d(st, row, data + k0 * data_stride, data_stride, len, n,
-                                     hipMemcpyHostToDevice, c->stream));
-        BchArgs a{st, row, len, st + len, row, nullptr, nullptr, 0, n, 0};
-        HIP_TRY(launch_encode(c->dev, a, c->stream));
-        HIP_TRY(ezrs::copy2d(ecc + k0 * ecc_stride, ecc_stride, st + len, row, eb, n,
-                                 hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
-    }
-    return 0;
+    return bch_encode_host_core(c, data, data_stride, len, ecc, ecc_stride, ncw, chunk);
+}
+
+int ezbch_encode_rows_host(ezbch_codec *c, uint8_t *rows, size_t stride, unsigned len, size_t ncw,
+                           size_t chunk) {
+    if (!c) return -EINVAL;
+    if (ncw == 0) return 0;
+    if (int r = check_rows(c, rows, stride, len, ncw)) return r;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    return bch_encode_host_core(c, rows, stride, len, rows + len, stride, ncw, chunk);
 }
 
 int ezbch_decode_host(ezbch_codec *c, uint8_t *data, size_t data_stride, unsigned len,
@@ -773,8 +818,13 @@ int ezbch_decode_host(ezbch_codec *c, uint8_t *data, size_t data_stride, unsigne
     if (!c) return -EINVAL;
     if (ncw == 0) return 0;
     if (!result) return -EINVAL;
-    if (int r = check_rows(c, data, data_stride, len, ecc, ecc_stride, ncw)) return r;
-    if (errloc && errloc_stride < c->h.t) return -EINVAL;
+    if (!ecc) {
+        if (int r = check_rows(c, data, data_stride, len, ncw)) return r;
+        ecc = data + len;
+        ecc_stride = data_stride;
+    }
+    if (int r = check_args(c, data, data_stride, len, ecc, ecc_stride, ncw)) return r;
+    if (errloc && ncw > 1 && errloc_stride < c->h.t) return -EINVAL;
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard g(c->device);
     const size_t eb = c->h.ecc_bytes, row = (size_t)len + eb, T = c->h.t;
@@ -795,7 +845,7 @@ int ezbch_decode_host(ezbch_codec *c, uint8_t *data, size_t data_stride, unsigne
         if (errloc)   // copy-in/copy-out: entries the decode does not write keep their value
             HIP_TRY(ezrs::copy2d(dloc, T * 4, errloc + k0 * errloc_stride, errloc_stride * 4,
                                      T * 4, n, hipMemcpyHostToDevice, c->stream));
-        BchArgs a{st, row, len, st + len, row, dres, errloc ? dloc : nullptr, T, n, 0};
+        BchArgs a{st, st, row, len, st + len, row, dres, errloc ? dloc : nullptr, T, n, 0};
         HIP_TRY(launch_decode(c->dev, a, c->stream));
         if (len)
             HIP_TRY(ezrs::copy2d(data + k0 * data_stride, data_stride, st, row, len, n,

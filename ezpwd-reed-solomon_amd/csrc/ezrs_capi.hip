@@ -10,6 +10,8 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <unordered_map>
+#include <vector>
 
 #include "../../include/ezrs.h"
 #include "ezrs_internal.hpp"
@@ -25,11 +27,21 @@ struct ezrs_codec {
     std::mutex mu;                // guards the lazily grown host-pipeline buffers
     void *h_stage[2] = {nullptr, nullptr};
     void *d_stage[2] = {nullptr, nullptr};
-    size_t stage_bytes = 0;
+    size_t stage_bytes = 0;       // device bytes of each d_stage buffer
+    size_t hstage_bytes = 0;      // pinned host bytes of each h_stage buffer
     hipStream_t streams[2] = {nullptr, nullptr};
     int bs_id = -1;               // bit-sliced GF(2^8) kernel set, -1 if none
-    uint8_t *d_syn = nullptr;     // decode workspace: syndromes of flagged codewords, [ncw][32]
-    size_t syn_cap = 0;           // codewords the workspace can hold
+    // Device workspaces of the batch entry points, one per HIP stream: calls on different streams
+    // never share scratch memory, calls on one stream are ordered by the stream.  A workspace only
+    // grows; the buffer it replaces is kept until ezrs_destroy, so work already queued (or a
+    // captured graph) that still points at it stays valid.  No entry point synchronises the device.
+    struct Ws {
+        void *p = nullptr;
+        size_t bytes = 0;
+    };
+    mutable std::mutex ws_mu;
+    mutable std::unordered_map<void *, Ws> ws;
+    mutable std::vector<void *> ws_retired;
 };
 
 namespace {
@@ -93,6 +105,12 @@ int ezrs_create(ezrs_codec **out, unsigned symbol_bits, unsigned poly, unsigned 
         delete c;
         g_last_error = "invalid RS codec parameters";
         return -EINVAL;
+    }
+    if (symbol_bits > 8 && nroots > 256) {
+        // the wide-symbol kernels keep at most 256 parity symbols' working state per lane
+        delete c;
+        g_last_error = "RS codecs with symbols wider than 8 bits support at most 256 parity symbols";
+        return -ENOTSUP;
     }
     int ndev = 0;
     hipError_t e = hipGetDeviceCount(&ndev);
@@ -165,7 +183,8 @@ int ezrs_destroy(ezrs_codec *c) {
     DeviceGuard g(c->device);
     (void)hipFree(c->d_tabs);
     (void)hipFree(c->d_dual);
-    if (c->d_syn) (void)hipFree(c->d_syn);
+    for (auto &kv : c->ws) (void)hipFree(kv.second.p);
+    for (void *p : c->ws_retired) (void)hipFree(p);
     for (int i = 0; i < 2; ++i) {
         if (c->d_stage[i]) (void)hipFree(c->d_stage[i]);
         if (c->h_stage[i]) (void)hipHostFree(c->h_stage[i]);
@@ -193,18 +212,26 @@ int ezrs_get_info(const ezrs_codec *c, ezrs_info *info) {
 
 namespace {
 
-// Grow the flagged-codeword syndrome workspace (bit-sliced decode path only).
-int reserve_syn(ezrs_codec *c, size_t ncw) {
-    if (c->bs_id < 0 || ncw <= c->syn_cap) return 0;
-    DeviceGuard g(c->device);
-    if (c->d_syn) {
-        HIP_TRY(hipDeviceSynchronize());
-        (void)hipFree(c->d_syn);
-        c->d_syn = nullptr;
-        c->syn_cap = 0;
+// Device scratch bytes one batch call of ncw codewords needs (encode and decode alike).
+size_t ws_bytes_for(const ezrs_codec *c, size_t ncw) {
+    return c->bs_id >= 0 ? bs_encode_ws_bytes(ncw) : 0;   // >= ncw * 32 (decode's need)
+}
+
+// The calling stream's workspace, grown to at least `bytes` (see ezrs_codec::Ws).
+int stream_ws(const ezrs_codec *c, void *stream, size_t bytes, void **out) {
+    *out = nullptr;
+    if (!bytes) return 0;
+    std::lock_guard<std::mutex> lk(c->ws_mu);
+    ezrs_codec::Ws &w = c->ws[stream];
+    if (w.bytes < bytes) {
+        const size_t grow = w.bytes + w.bytes / 2 > bytes ? w.bytes + w.bytes / 2 : bytes;
+        void *p = nullptr;
+        HIP_TRY(hipMalloc(&p, grow));
+        if (w.p) c->ws_retired.push_back(w.p);
+        w.p = p;
+        w.bytes = grow;
     }
-    HIP_TRY(hipMalloc(&c->d_syn, bs_encode_ws_bytes(ncw)));   // >= ncw * 32 (decode's need)
-    c->syn_cap = ncw;
+    *out = w.p;
     return 0;
 }
 
@@ -236,41 +263,54 @@ hipError_t dispatch_decode(const ezrs_codec *c, const DecodeArgs &a, uint8_t *sy
 
 } // namespace
 
-int ezrs_reserve(ezrs_codec *c, size_t ncw) {
+int ezrs_reserve(ezrs_codec *c, size_t ncw) { return ezrs_reserve_stream(c, ncw, nullptr); }
+
+int ezrs_reserve_stream(const ezrs_codec *c, size_t ncw, void *stream) {
     if (!c) return -EINVAL;
-    return reserve_syn(c, ncw);
+    DeviceGuard g(c->device);
+    void *p;
+    return stream_ws(c, stream, ws_bytes_for(c, ncw), &p);
 }
 
-int ezrs_encode(const ezrs_codec *c, const void *data, size_t data_stride, unsigned len,
-                void *parity, size_t parity_stride, size_t ncw, void *stream) {
-    if (!c) return -EINVAL;
-    if (ncw == 0) return 0;
-    if (!data) return -EINVAL;
-    const unsigned w = c->dev.mm <= 8 ? 1 : 2;
+size_t ezrs_workspace_bytes(const ezrs_codec *c, size_t ncw) {
+    return c ? ws_bytes_for(c, ncw) : 0;
+}
+
+namespace {
+
+// Argument checks of encode<INP> (rs_base:868-904) for a batch with a separate parity array.
+int check_encode(const ezrs_codec *c, const void *data, size_t data_stride, unsigned len,
+                 const void *parity, size_t parity_stride, size_t ncw) {
+    if (!c || !data || !parity) return -EINVAL;
     if (len < 1 || len > c->dev.load) return -EINVAL;                 // rs_base:875-877
-    if (!parity) {
-        parity = static_cast<char *>(const_cast<void *>(data)) + (size_t)len * w;
-        parity_stride = data_stride;
-        if (data_stride < (size_t)len + c->dev.nroots && ncw > 1) return -EINVAL;
-    } else if (ncw > 1 && parity_stride < c->dev.nroots) {
-        return -EINVAL;
-    }
-    if (ncw > 1 && data_stride < len) return -EINVAL;
+    if (ncw > 1 && (parity_stride < c->dev.nroots || data_stride < len)) return -EINVAL;
+    return 0;
+}
+
+// Row form (rs_base:778-790): the parity follows the data in each row.
+int check_rows(const ezrs_codec *c, const void *rows, size_t stride, unsigned len, size_t ncw) {
+    if (!c || !rows) return -EINVAL;
+    if (len < 1 || len > c->dev.load) return -EINVAL;
+    if (ncw > 1 && stride < (size_t)len + c->dev.nroots) return -EINVAL;
+    return 0;
+}
+
+int encode_dev(const ezrs_codec *c, const void *data, size_t data_stride, unsigned len,
+               void *parity, size_t parity_stride, size_t ncw, void *ws, size_t ws_bytes,
+               void *stream) {
+    if (ws_bytes < ws_bytes_for(c, ncw) || (ws_bytes && !ws)) return -EINVAL;
     DeviceGuard g(c->device);
     EncodeArgs a{data, data_stride, len, parity, parity_stride, ncw};
-    if (int r = reserve_syn(const_cast<ezrs_codec *>(c), ncw)) return r;
-    hipError_t e = dispatch_encode(c, a, c->d_syn, static_cast<hipStream_t>(stream));
+    hipError_t e = dispatch_encode(c, a, ws, static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return hip_fail(e, "encode launch");
     return 0;
 }
 
-int ezrs_decode(const ezrs_codec *c, void *data, size_t data_stride, unsigned len, void *parity,
-                size_t parity_stride, const uint32_t *eras, size_t eras_stride,
-                const uint32_t *neras, int32_t *result, uint32_t *positions, size_t pos_stride,
-                void *corr, size_t corr_stride, size_t ncw, void *stream) {
-    if (!c) return -EINVAL;
-    if (ncw == 0) return 0;
-    if (!data || !result) return -EINVAL;
+int check_decode(const ezrs_codec *c, void *data, size_t data_stride, unsigned len,
+                 void *&parity, size_t &parity_stride, const uint32_t *eras, size_t eras_stride,
+                 const uint32_t *neras, int32_t *result, uint32_t *positions, size_t pos_stride,
+                 void *corr, size_t corr_stride, size_t ncw) {
+    if (!c || !data || !result) return -EINVAL;
     const unsigned w = c->dev.mm <= 8 ? 1 : 2;
     const unsigned NR = c->dev.nroots;
     if (len < 1 || len > c->dev.load) return -EINVAL;
@@ -283,41 +323,187 @@ int ezrs_decode(const ezrs_codec *c, void *data, size_t data_stride, unsigned le
     }
     if (ncw > 1 && data_stride < len) return -EINVAL;
     if (neras && !eras) return -EINVAL;
+    if (eras && ncw > 1 && eras_stride == 0) return -EINVAL;
     if (positions && ncw > 1 && pos_stride < NR) return -EINVAL;
     if (corr && ncw > 1 && corr_stride < NR) return -EINVAL;
+    return 0;
+}
+
+} // namespace
+
+int ezrs_encode_ws(const ezrs_codec *c, const void *data, size_t data_stride, unsigned len,
+                   void *parity, size_t parity_stride, size_t ncw, void *ws, size_t ws_bytes,
+                   void *stream) {
+    if (!c) return -EINVAL;
+    if (ncw == 0) return 0;
+    if (int r = check_encode(c, data, data_stride, len, parity, parity_stride, ncw)) return r;
+    return encode_dev(c, data, data_stride, len, parity, parity_stride, ncw, ws, ws_bytes, stream);
+}
+
+int ezrs_encode(const ezrs_codec *c, const void *data, size_t data_stride, unsigned len,
+                void *parity, size_t parity_stride, size_t ncw, void *stream) {
+    if (!c) return -EINVAL;
+    if (ncw == 0) return 0;
+    if (int r = check_encode(c, data, data_stride, len, parity, parity_stride, ncw)) return r;
     DeviceGuard g(c->device);
+    const size_t need = ws_bytes_for(c, ncw);
+    void *ws = nullptr;
+    if (int r = stream_ws(c, stream, need, &ws)) return r;
+    return encode_dev(c, data, data_stride, len, parity, parity_stride, ncw, ws, need, stream);
+}
+
+int ezrs_encode_rows_ws(const ezrs_codec *c, void *rows, size_t stride, unsigned len, size_t ncw,
+                        void *ws, size_t ws_bytes, void *stream) {
+    if (!c) return -EINVAL;
+    if (ncw == 0) return 0;
+    if (int r = check_rows(c, rows, stride, len, ncw)) return r;
+    char *r0 = static_cast<char *>(rows);
+    const size_t w = c->dev.mm <= 8 ? 1 : 2;
+    return encode_dev(c, r0, stride, len, r0 + (size_t)len * w, stride, ncw, ws, ws_bytes, stream);
+}
+
+int ezrs_encode_rows(const ezrs_codec *c, void *rows, size_t stride, unsigned len, size_t ncw,
+                     void *stream) {
+    if (!c) return -EINVAL;
+    if (ncw == 0) return 0;
+    if (int r = check_rows(c, rows, stride, len, ncw)) return r;
+    DeviceGuard g(c->device);
+    const size_t need = ws_bytes_for(c, ncw);
+    void *ws = nullptr;
+    if (int r = stream_ws(c, stream, need, &ws)) return r;
+    return ezrs_encode_rows_ws(c, rows, stride, len, ncw, ws, need, stream);
+}
+
+int ezrs_decode_ws(const ezrs_codec *c, void *data, size_t data_stride, unsigned len,
+                   void *parity, size_t parity_stride, const uint32_t *eras, size_t eras_stride,
+                   const uint32_t *neras, int32_t *result, uint32_t *positions, size_t pos_stride,
+                   void *corr, size_t corr_stride, size_t ncw, void *ws, size_t ws_bytes,
+                   void *stream) {
+    if (!c) return -EINVAL;
+    if (ncw == 0) return 0;
+    if (int r = check_decode(c, data, data_stride, len, parity, parity_stride, eras, eras_stride,
+                             neras, result, positions, pos_stride, corr, corr_stride, ncw))
+        return r;
+    if (ws_bytes < ws_bytes_for(c, ncw) || (ws_bytes && !ws)) return -EINVAL;
+    DeviceGuard g(c->device);
+    // one codeword: a zero eras_stride is harmless (row 0 only)
     DecodeArgs a{data, data_stride, len, parity, parity_stride, eras, eras_stride, neras,
                  result, positions, pos_stride, corr, corr_stride, ncw};
-    if (int r = reserve_syn(const_cast<ezrs_codec *>(c), ncw)) return r;
-    hipError_t e = dispatch_decode(c, a, c->d_syn, static_cast<hipStream_t>(stream));
+    hipError_t e = dispatch_decode(c, a, static_cast<uint8_t *>(ws), static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return hip_fail(e, "decode launch");
     return 0;
+}
+
+int ezrs_decode(const ezrs_codec *c, void *data, size_t data_stride, unsigned len, void *parity,
+                size_t parity_stride, const uint32_t *eras, size_t eras_stride,
+                const uint32_t *neras, int32_t *result, uint32_t *positions, size_t pos_stride,
+                void *corr, size_t corr_stride, size_t ncw, void *stream) {
+    if (!c) return -EINVAL;
+    if (ncw == 0) return 0;
+    DeviceGuard g(c->device);
+    const size_t need = ws_bytes_for(c, ncw);
+    void *ws = nullptr;
+    if (int r = stream_ws(c, stream, need, &ws)) return r;
+    return ezrs_decode_ws(c, data, data_stride, len, parity, parity_stride, eras, eras_stride,
+                          neras, result, positions, pos_stride, corr, corr_stride, ncw, ws, need,
+                          stream);
 }
 
 // ---- host-memory pipeline ---------------------------------------------------------------------
 namespace {
 
-int ensure_stage(ezrs_codec *c, size_t bytes) {
+// Device and pinned-host staging of the host-memory forms: two sets (one per pipeline stream).
+int ensure_stage(ezrs_codec *c, size_t dbytes, size_t hbytes) {
     if (!c->streams[0])
         for (int i = 0; i < 2; ++i)
             HIP_TRY(hipStreamCreateWithFlags(&c->streams[i], hipStreamNonBlocking));
-    if (c->stage_bytes >= bytes) return 0;
-    for (int i = 0; i < 2; ++i) {
-        if (c->d_stage[i]) (void)hipFree(c->d_stage[i]);
-        c->d_stage[i] = nullptr;
+    if (c->stage_bytes < dbytes) {
+        for (int i = 0; i < 2; ++i) {
+            if (c->d_stage[i]) (void)hipFree(c->d_stage[i]);
+            c->d_stage[i] = nullptr;
+        }
+        c->stage_bytes = 0;
+        for (int i = 0; i < 2; ++i) HIP_TRY(hipMalloc(&c->d_stage[i], dbytes));
+        c->stage_bytes = dbytes;
     }
-    c->stage_bytes = 0;
-    for (int i = 0; i < 2; ++i) HIP_TRY(hipMalloc(&c->d_stage[i], bytes));
-    c->stage_bytes = bytes;
+    if (c->hstage_bytes < hbytes) {
+        for (int i = 0; i < 2; ++i) {
+            if (c->h_stage[i]) (void)hipHostFree(c->h_stage[i]);
+            c->h_stage[i] = nullptr;
+        }
+        c->hstage_bytes = 0;
+        for (int i = 0; i < 2; ++i) HIP_TRY(hipHostMalloc(&c->h_stage[i], hbytes, hipHostMallocDefault));
+        c->hstage_bytes = hbytes;
+    }
     return 0;
 }
 
 size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
 size_t default_chunk(size_t row_bytes) {
-    const size_t target = (size_t)64 << 20;  // 64 MiB of codewords per chunk
+    const size_t target = (size_t)64 << 20;  // 64 MiB of staged rows per chunk
     size_t n = target / (row_bytes ? row_bytes : 1);
     return n ? n : 1;
+}
+
+// Encode of host rows.  PCIe traffic: the rows' data symbols go to the device (one linear copy
+// of the rows' span when the row pitch is at most twice what a row needs, otherwise a CPU gather
+// into pinned staging first), the kernel writes the parity as one compact [n][NR] block, and only
+// that block comes back (a linear copy; a CPU scatter puts each row's NR symbols in place unless
+// the caller's parity array is itself compact).  The caller's data symbols are never written.
+//   rows != NULL: the rs_base:778-790 row form, parity at rows + len (data is rows)
+int encode_host_core(ezrs_codec *c, const char *data, size_t data_stride, unsigned len,
+                     char *parity, size_t parity_stride, size_t ncw, size_t chunk) {
+    const size_t w = c->dev.mm <= 8 ? 1 : 2, NR = c->dev.nroots;
+    const size_t need = (size_t)len;                               // symbols a row must carry over
+    const bool span = ncw == 1 || data_stride <= 2 * need + NR;    // linear copy of the rows' span
+    const size_t drow = span ? data_stride : need;                 // device row pitch (symbols)
+    const bool par_direct = parity_stride == NR || ncw == 1;       // caller's parity is compact
+    if (!chunk) chunk = default_chunk(drow * w);
+    if (chunk > ncw) chunk = ncw;
+    const size_t b_in = align_up(chunk * drow * w), b_par = align_up(chunk * NR * w),
+                 b_ws = align_up(ws_bytes_for(c, chunk));
+    const size_t h_in = span ? 0 : align_up(chunk * need * w), h_par = par_direct ? 0 : b_par;
+    if (int r = ensure_stage(c, b_in + b_par + b_ws, h_in + h_par + 256)) return r;
+    struct Pending { size_t k0 = 0, n = 0; bool live = false; } pend[2];
+    auto scatter = [&](int s) {
+        if (!pend[s].live || par_direct) return;
+        const char *src = static_cast<const char *>(c->h_stage[s]) + h_in;
+        for (size_t r = 0; r < pend[s].n; ++r)
+            std::memcpy(parity + (pend[s].k0 + r) * parity_stride * w, src + r * NR * w, NR * w);
+    };
+    for (size_t i = 0, k0 = 0; k0 < ncw; ++i, k0 += chunk) {
+        const int s = (int)(i & 1);
+        hipStream_t st = c->streams[s];
+        const size_t n = ncw - k0 < chunk ? ncw - k0 : chunk;
+        if (pend[s].live) {
+            HIP_TRY(hipStreamSynchronize(st));
+            scatter(s);
+            pend[s].live = false;
+        }
+        char *d_in = static_cast<char *>(c->d_stage[s]), *d_par = d_in + b_in, *d_ws = d_par + b_par;
+        char *hs = static_cast<char *>(c->h_stage[s]);
+        const char *hd = data + k0 * data_stride * w;
+        if (span) {
+            HIP_TRY(hipMemcpyAsync(d_in, hd, ((n - 1) * data_stride + need) * w,
+                                   hipMemcpyHostToDevice, st));
+        } else {
+            for (size_t r = 0; r < n; ++r) std::memcpy(hs + r * need * w, hd + r * data_stride * w, need * w);
+            HIP_TRY(hipMemcpyAsync(d_in, hs, n * need * w, hipMemcpyHostToDevice, st));
+        }
+        EncodeArgs a{d_in, drow, len, d_par, NR, n};
+        HIP_TRY(dispatch_encode(c, a, d_ws, st));
+        if (par_direct)
+            HIP_TRY(hipMemcpyAsync(parity + k0 * NR * w, d_par, n * NR * w, hipMemcpyDeviceToHost, st));
+        else
+            HIP_TRY(hipMemcpyAsync(hs + h_in, d_par, n * NR * w, hipMemcpyDeviceToHost, st));
+        pend[s] = {k0, n, true};
+    }
+    for (int s = 0; s < 2; ++s) {
+        HIP_TRY(hipStreamSynchronize(c->streams[s]));
+        scatter(s);
+    }
+    return 0;
 }
 
 } // namespace
@@ -326,57 +512,28 @@ int ezrs_encode_host(ezrs_codec *c, const void *data, size_t data_stride, unsign
                      void *parity, size_t parity_stride, size_t ncw, size_t chunk) {
     if (!c) return -EINVAL;
     if (ncw == 0) return 0;
-    if (!data) return -EINVAL;
-    const unsigned w = c->dev.mm <= 8 ? 1 : 2, NR = c->dev.nroots;
-    if (len < 1 || len > c->dev.load) return -EINVAL;
-    if (!parity) {
-        parity = static_cast<char *>(const_cast<void *>(data)) + (size_t)len * w;
-        parity_stride = data_stride;
+    if (int r = check_encode(c, data, data_stride, len, parity, parity_stride, ncw)) {
+        if (!parity)
+            g_last_error = "ezrs_encode_host: parity is required (rows that carry their own parity: "
+                           "ezrs_encode_rows_host)";
+        return r;
     }
-    if (ncw > 1 && (data_stride < len || parity_stride < NR)) return -EINVAL;
-    // Parity inside the row (the common RS<N,K> layout): move whole rows with one linear copy per
-    // chunk instead of a 2-D copy of ncw short rows (2-D copies from pageable memory go row by row).
-    const bool inline_par = parity_stride == data_stride && data_stride >= (size_t)len + NR &&
-                            static_cast<const char *>(parity) ==
-                                static_cast<const char *>(data) + (size_t)len * w;
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard g(c->device);
-    const size_t drow = inline_par ? data_stride : len;      // device row stride, symbols
-    if (!chunk) chunk = default_chunk((size_t)(len + NR) * w);
-    if (chunk > ncw) chunk = ncw;
-    const size_t dbytes = align_up(chunk * drow * w), pbytes = align_up(chunk * NR * w),
-                 wbytes = c->bs_id >= 0 ? align_up(bs_encode_ws_bytes(chunk)) : 0;
-    if (int r = ensure_stage(c, dbytes + pbytes + wbytes)) return r;
-    for (size_t i = 0, k0 = 0; k0 < ncw; ++i, k0 += chunk) {
-        const int s = (int)(i & 1);
-        hipStream_t st = c->streams[s];
-        const size_t n = ncw - k0 < chunk ? ncw - k0 : chunk;
-        if (i >= 2) HIP_TRY(hipStreamSynchronize(st));
-        char *dd = static_cast<char *>(c->d_stage[s]), *dp = dd + dbytes;
-        const char *hd = static_cast<const char *>(data) + k0 * data_stride * w;
-        char *hp = static_cast<char *>(parity) + k0 * parity_stride * w;
-        if (inline_par) {
-            // the last row's tail past its parity may lie outside the caller's buffer
-            HIP_TRY(hipMemcpyAsync(dd, hd, ((n - 1) * data_stride + len + NR) * w,
-                                   hipMemcpyHostToDevice, st));
-            EncodeArgs a{dd, data_stride, len, dd + (size_t)len * w, data_stride, n};
-            HIP_TRY(dispatch_encode(c, a, dp + pbytes, st));
-            // Rows go back whole: a 2-D copy of NR-symbol pieces at row pitch runs row by row
-            // (6.8 s for 1M RS(255,223) rows, pinned or not); the data bytes written back are
-            // the ones just read, unchanged.
-            HIP_TRY(hipMemcpyAsync(const_cast<char *>(hd), dd, ((n - 1) * data_stride + len + NR) * w,
-                                   hipMemcpyDeviceToHost, st));
-            continue;
-        }
-        HIP_TRY(ezrs::copy2d(dd, (size_t)len * w, hd, data_stride * w, (size_t)len * w, n,
-                                 hipMemcpyHostToDevice, st));
-        EncodeArgs a{dd, len, len, dp, NR, n};
-        HIP_TRY(dispatch_encode(c, a, dp + pbytes, st));
-        HIP_TRY(ezrs::copy2d(hp, parity_stride * w, dp, (size_t)NR * w, (size_t)NR * w, n,
-                                 hipMemcpyDeviceToHost, st));
-    }
-    for (int s = 0; s < 2; ++s) HIP_TRY(hipStreamSynchronize(c->streams[s]));
-    return 0;
+    return encode_host_core(c, static_cast<const char *>(data), data_stride, len,
+                            static_cast<char *>(parity), parity_stride, ncw, chunk);
+}
+
+int ezrs_encode_rows_host(ezrs_codec *c, void *rows, size_t stride, unsigned len, size_t ncw,
+                          size_t chunk) {
+    if (!c) return -EINVAL;
+    if (ncw == 0) return 0;
+    if (int r0 = check_rows(c, rows, stride, len, ncw)) return r0;
+    const size_t w = c->dev.mm <= 8 ? 1 : 2;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    char *r = static_cast<char *>(rows);
+    return encode_host_core(c, r, stride, len, r + (size_t)len * w, stride, ncw, chunk);
 }
 
 int ezrs_decode_host(ezrs_codec *c, void *data, size_t data_stride, unsigned len, void *parity,
@@ -396,8 +553,12 @@ int ezrs_decode_host(ezrs_codec *c, void *data, size_t data_stride, unsigned len
     if (neras && !eras) return -EINVAL;
     if (positions && ncw > 1 && pos_stride < NR) return -EINVAL;
     if (corr && ncw > 1 && corr_stride < NR) return -EINVAL;
-    const size_t ecols = eras ? (eras_stride < NR ? eras_stride : NR) : 0;
+    // erasure columns to stage: the row stride (capped at NR); a single codeword may pass
+    // eras_stride 0, and then carries neras[0] entries
+    size_t ecols = eras ? (eras_stride < NR ? eras_stride : NR) : 0;
+    if (eras && ncw == 1 && eras_stride == 0) ecols = neras ? (neras[0] < NR ? neras[0] : NR) : 0;
     if (eras && ecols == 0 && ncw > 1) return -EINVAL;
+    if (eras && ecols == 0) eras = nullptr, neras = nullptr;
     const bool inline_par = parity_stride == data_stride && data_stride >= (size_t)len + NR &&
                             static_cast<const char *>(parity) ==
                                 static_cast<const char *>(data) + (size_t)len * w;
@@ -411,8 +572,8 @@ int ezrs_decode_host(ezrs_codec *c, void *data, size_t data_stride, unsigned len
                  b_ne = align_up(neras ? chunk * 4 : 0), b_rs = align_up(chunk * 4),
                  b_ps = align_up(positions ? chunk * NR * 4 : 0),
                  b_co = align_up(corr ? chunk * NR * w : 0),
-                 b_sy = align_up(c->bs_id >= 0 ? chunk * 32 : 0);
-    if (int r = ensure_stage(c, b_cw + b_er + b_ne + b_rs + b_ps + b_co + b_sy)) return r;
+                 b_sy = align_up(ws_bytes_for(c, chunk));
+    if (int r = ensure_stage(c, b_cw + b_er + b_ne + b_rs + b_ps + b_co + b_sy, 0)) return r;
     for (size_t i = 0, k0 = 0; k0 < ncw; ++i, k0 += chunk) {
         const int s = (int)(i & 1);
         hipStream_t st = c->streams[s];

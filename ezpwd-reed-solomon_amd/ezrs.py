@@ -63,10 +63,19 @@ def lib():
         L.ezrs_destroy.argtypes = [_vp]
         L.ezrs_get_info.argtypes = [_vp, C.POINTER(Info)]
         L.ezrs_reserve.argtypes = [_vp, _sz]
+        L.ezrs_reserve_stream.argtypes = [_vp, _sz, _vp]
+        L.ezrs_workspace_bytes.argtypes = [_vp, _sz]
+        L.ezrs_workspace_bytes.restype = _sz
         L.ezrs_encode.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _sz, _vp]
+        L.ezrs_encode_rows.argtypes = [_vp, _vp, _sz, _u, _sz, _vp]
+        L.ezrs_encode_ws.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _sz, _vp, _sz, _vp]
+        L.ezrs_encode_rows_ws.argtypes = [_vp, _vp, _sz, _u, _sz, _vp, _sz, _vp]
         L.ezrs_decode.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _vp, _sz, _vp, _vp, _vp, _sz,
                                   _vp, _sz, _sz, _vp]
+        L.ezrs_decode_ws.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _vp, _sz, _vp, _vp, _vp, _sz,
+                                     _vp, _sz, _sz, _vp, _sz, _vp]
         L.ezrs_encode_host.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _sz, _sz]
+        L.ezrs_encode_rows_host.argtypes = [_vp, _vp, _sz, _u, _sz, _sz]
         L.ezrs_decode_host.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _vp, _sz, _vp, _vp, _vp,
                                        _sz, _vp, _sz, _sz, _sz]
         L.ezrs_host_alloc.argtypes = [C.POINTER(_vp), _sz]
@@ -77,6 +86,8 @@ def lib():
         L.ezbch_destroy.argtypes = [_vp]
         L.ezbch_get_info.argtypes = [_vp, C.POINTER(BCHInfo)]
         L.ezbch_encode.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _sz, _vp]
+        L.ezbch_encode_rows.argtypes = [_vp, _vp, _sz, _u, _sz, _vp]
+        L.ezbch_encode_rows_host.argtypes = [_vp, _vp, _sz, _u, _sz, _sz]
         L.ezbch_decode.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _vp, _vp, _sz, _sz, _vp]
         L.ezbch_encode_host.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _sz, _sz]
         L.ezbch_decode_host.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _vp, _vp, _sz, _sz, _sz]
@@ -98,6 +109,41 @@ def _tp(t):
 
 def _np(a):
     return None if a is None else a.ctypes.data_as(_vp)
+
+
+_ITEM = {"uint8": 1, "int8": 1, "uint16": 2, "int16": 2, "uint32": 4, "int32": 4}
+
+
+def _dev_rows(t, what, device, itemsize, ndim=2):
+    """Validate a device tensor argument: on the codec's device, rows of contiguous elements of the
+    expected width; returns its row stride in elements (0 for None)."""
+    if t is None:
+        return 0
+    if not getattr(t, "is_cuda", False):
+        raise EzrsError(f"{what}: expected a GPU tensor")
+    if t.device.index != device:
+        raise EzrsError(f"{what}: tensor on cuda:{t.device.index}, codec on cuda:{device}")
+    if t.element_size() != itemsize:
+        raise EzrsError(f"{what}: expected {itemsize}-byte elements, got {t.dtype}")
+    if t.dim() != ndim or (ndim == 2 and t.shape[1] > 1 and t.stride(1) != 1):
+        raise EzrsError(f"{what}: expected a {ndim}-D tensor with contiguous rows")
+    return t.stride(0) if ndim == 2 else 1
+
+
+def _host_rows(a, what, itemsize, ndim=2):
+    """Validate a numpy argument of the host forms; returns its row stride in elements."""
+    if a is None:
+        return 0
+    if not isinstance(a, np.ndarray):
+        raise EzrsError(f"{what}: expected a numpy array")
+    if a.itemsize != itemsize:
+        raise EzrsError(f"{what}: expected {itemsize}-byte elements, got {a.dtype}")
+    if a.ndim != ndim or (ndim == 2 and a.shape[1] > 1 and a.strides[1] != itemsize) or \
+            (ndim == 2 and a.strides[0] % itemsize):
+        raise EzrsError(f"{what}: expected a {ndim}-D array with contiguous rows")
+    if ndim == 1 and a.strides[0] != itemsize:
+        raise EzrsError(f"{what}: expected a contiguous array")
+    return a.strides[0] // itemsize if ndim == 2 else 1
 
 
 def _stream_ptr(stream):
@@ -157,56 +203,82 @@ class Codec:
         import torch
         return torch.uint8 if self.dtype == np.uint8 else torch.uint16
 
-    def reserve(self, ncw):
-        _check(lib().ezrs_reserve(self._h, ncw), "ezrs_reserve")
+    def reserve(self, ncw, stream=None):
+        """Pre-size the workspace of `stream` (default: the current torch stream)."""
+        _check(lib().ezrs_reserve_stream(self._h, ncw, _stream_ptr(stream)), "ezrs_reserve_stream")
+
+    def workspace_bytes(self, ncw):
+        return int(lib().ezrs_workspace_bytes(self._h, ncw))
 
     # -- device batch forms ------------------------------------------------------------------
     def encode(self, data, length=None, parity=None, stream=None):
-        """data: [ncw, stride] device tensor; parity: [ncw, >=nroots] or None (parity written
-        into columns length..length+nroots of data)."""
-        ncw, stride = data.shape
-        length = stride - self.nroots if length is None else length
-        ps = parity.stride(0) if parity is not None else 0
-        _check(lib().ezrs_encode(self._h, _tp(data), data.stride(0), length, _tp(parity), ps,
-                                 ncw, _stream_ptr(stream)), "ezrs_encode")
+        """data: [ncw, stride] device tensor; parity: [ncw, >=nroots] tensor, or None: each row
+        carries its parity in columns length..length+nroots (ezrs_encode_rows)."""
+        w = self.info.datum_bytes
+        ncw = data.shape[0]
+        ds = _dev_rows(data, "data", self.device, w)
+        ps = _dev_rows(parity, "parity", self.device, w)
+        length = data.shape[1] - self.nroots if length is None else length
+        if parity is None:
+            _check(lib().ezrs_encode_rows(self._h, _tp(data), ds, length, ncw, _stream_ptr(stream)),
+                   "ezrs_encode_rows")
+        else:
+            _check(lib().ezrs_encode(self._h, _tp(data), ds, length, _tp(parity), ps, ncw,
+                                     _stream_ptr(stream)), "ezrs_encode")
 
     def decode(self, data, length=None, parity=None, eras=None, neras=None, result=None,
                positions=None, corr=None, stream=None):
         """In-place batch decode; returns the int32 result tensor."""
         import torch
-        ncw, stride = data.shape
-        length = stride - self.nroots if length is None else length
+        w = self.info.datum_bytes
+        ncw = data.shape[0]
+        ds = _dev_rows(data, "data", self.device, w)
+        ps = _dev_rows(parity, "parity", self.device, w)
+        es = _dev_rows(eras, "eras", self.device, 4)
+        _dev_rows(neras, "neras", self.device, 4, ndim=1)
+        qs = _dev_rows(positions, "positions", self.device, 4)
+        cs = _dev_rows(corr, "corr", self.device, w)
+        length = data.shape[1] - self.nroots if length is None else length
         if result is None:
             result = torch.empty(ncw, dtype=torch.int32, device=data.device)
+        _dev_rows(result, "result", self.device, 4, ndim=1)
         _check(lib().ezrs_decode(
-            self._h, _tp(data), data.stride(0), length, _tp(parity),
-            parity.stride(0) if parity is not None else 0,
-            _tp(eras), eras.stride(0) if eras is not None else 0, _tp(neras), _tp(result),
-            _tp(positions), positions.stride(0) if positions is not None else 0,
-            _tp(corr), corr.stride(0) if corr is not None else 0, ncw, _stream_ptr(stream)),
+            self._h, _tp(data), ds, length, _tp(parity), ps, _tp(eras), es, _tp(neras),
+            _tp(result), _tp(positions), qs, _tp(corr), cs, ncw, _stream_ptr(stream)),
             "ezrs_decode")
         return result
 
     # -- host batch forms ----------------------------------------------------------------------
     def encode_host(self, data, length=None, parity=None, chunk=0):
-        ncw, stride = data.shape
-        length = stride - self.nroots if length is None else length
-        ps = parity.shape[1] if parity is not None else 0
-        _check(lib().ezrs_encode_host(self._h, _np(data), stride, length, _np(parity), ps, ncw,
-                                      chunk), "ezrs_encode_host")
+        """data: [ncw, stride] numpy rows (only read); parity: [ncw, >=nroots] array, or None:
+        each row carries its parity after its data (ezrs_encode_rows_host)."""
+        w = self.info.datum_bytes
+        ncw = data.shape[0]
+        ds = _host_rows(data, "data", w)
+        ps = _host_rows(parity, "parity", w)
+        length = data.shape[1] - self.nroots if length is None else length
+        if parity is None:
+            _check(lib().ezrs_encode_rows_host(self._h, _np(data), ds, length, ncw, chunk),
+                   "ezrs_encode_rows_host")
+        else:
+            _check(lib().ezrs_encode_host(self._h, _np(data), ds, length, _np(parity), ps, ncw,
+                                          chunk), "ezrs_encode_host")
 
     def decode_host(self, data, length=None, parity=None, eras=None, neras=None,
                     positions=None, corr=None, chunk=0):
-        ncw, stride = data.shape
-        length = stride - self.nroots if length is None else length
+        w = self.info.datum_bytes
+        ncw = data.shape[0]
+        ds = _host_rows(data, "data", w)
+        ps = _host_rows(parity, "parity", w)
+        es = _host_rows(eras, "eras", 4)
+        _host_rows(neras, "neras", 4, ndim=1)
+        qs = _host_rows(positions, "positions", 4)
+        cs = _host_rows(corr, "corr", w)
+        length = data.shape[1] - self.nroots if length is None else length
         result = np.zeros(ncw, np.int32)
         _check(lib().ezrs_decode_host(
-            self._h, _np(data), stride, length, _np(parity),
-            parity.shape[1] if parity is not None else 0,
-            _np(eras), eras.shape[1] if eras is not None else 0, _np(neras), _np(result),
-            _np(positions), positions.shape[1] if positions is not None else 0,
-            _np(corr), corr.shape[1] if corr is not None else 0, ncw, chunk),
-            "ezrs_decode_host")
+            self._h, _np(data), ds, length, _np(parity), ps, _np(eras), es, _np(neras),
+            _np(result), _np(positions), qs, _np(corr), cs, ncw, chunk), "ezrs_decode_host")
         return result
 
 
@@ -256,41 +328,54 @@ class BCH:
         return (self.n - self.ecc_bits) // 8
 
     def encode(self, data, length=None, ecc=None, stream=None):
-        """data: [ncw, stride] uint8 device tensor; ecc: [ncw, >=ecc_bytes] or None (the ECC goes
-        to columns length..length+ecc_bytes of data)."""
-        ncw, stride = data.shape
-        length = stride - self.ecc_bytes if length is None else length
-        _check(lib().ezbch_encode(self._h, _tp(data), data.stride(0), length, _tp(ecc),
-                                  ecc.stride(0) if ecc is not None else 0, ncw,
-                                  _stream_ptr(stream)), "ezbch_encode", True)
+        """data: [ncw, stride] uint8 device tensor; ecc: [ncw, >=ecc_bytes] tensor, or None: the ECC
+        goes to columns length..length+ecc_bytes of each row (ezbch_encode_rows)."""
+        ncw = data.shape[0]
+        ds = _dev_rows(data, "data", self.device, 1)
+        es = _dev_rows(ecc, "ecc", self.device, 1)
+        length = data.shape[1] - self.ecc_bytes if length is None else length
+        if ecc is None:
+            _check(lib().ezbch_encode_rows(self._h, _tp(data), ds, length, ncw, _stream_ptr(stream)),
+                   "ezbch_encode_rows", True)
+        else:
+            _check(lib().ezbch_encode(self._h, _tp(data), ds, length, _tp(ecc), es, ncw,
+                                      _stream_ptr(stream)), "ezbch_encode", True)
 
     def decode(self, data, length=None, ecc=None, result=None, errloc=None, stream=None):
         import torch
-        ncw, stride = data.shape
-        length = stride - self.ecc_bytes if length is None else length
+        ncw = data.shape[0]
+        ds = _dev_rows(data, "data", self.device, 1)
+        es = _dev_rows(ecc, "ecc", self.device, 1)
+        ls = _dev_rows(errloc, "errloc", self.device, 4)
+        length = data.shape[1] - self.ecc_bytes if length is None else length
         if result is None:
             result = torch.empty(ncw, dtype=torch.int32, device=data.device)
-        _check(lib().ezbch_decode(self._h, _tp(data), data.stride(0), length, _tp(ecc),
-                                  ecc.stride(0) if ecc is not None else 0, _tp(result),
-                                  _tp(errloc), errloc.stride(0) if errloc is not None else 0, ncw,
-                                  _stream_ptr(stream)), "ezbch_decode", True)
+        _dev_rows(result, "result", self.device, 4, ndim=1)
+        _check(lib().ezbch_decode(self._h, _tp(data), ds, length, _tp(ecc), es, _tp(result),
+                                  _tp(errloc), ls, ncw, _stream_ptr(stream)), "ezbch_decode", True)
         return result
 
     def encode_host(self, data, length=None, ecc=None, chunk=0):
-        ncw, stride = data.shape
-        length = stride - self.ecc_bytes if length is None else length
-        _check(lib().ezbch_encode_host(self._h, _np(data), stride, length, _np(ecc),
-                                       ecc.shape[1] if ecc is not None else 0, ncw, chunk),
-               "ezbch_encode_host", True)
+        ncw = data.shape[0]
+        ds = _host_rows(data, "data", 1)
+        es = _host_rows(ecc, "ecc", 1)
+        length = data.shape[1] - self.ecc_bytes if length is None else length
+        if ecc is None:
+            _check(lib().ezbch_encode_rows_host(self._h, _np(data), ds, length, ncw, chunk),
+                   "ezbch_encode_rows_host", True)
+        else:
+            _check(lib().ezbch_encode_host(self._h, _np(data), ds, length, _np(ecc), es, ncw, chunk),
+                   "ezbch_encode_host", True)
 
     def decode_host(self, data, length=None, ecc=None, errloc=None, chunk=0):
-        ncw, stride = data.shape
-        length = stride - self.ecc_bytes if length is None else length
+        ncw = data.shape[0]
+        ds = _host_rows(data, "data", 1)
+        es = _host_rows(ecc, "ecc", 1)
+        ls = _host_rows(errloc, "errloc", 4)
+        length = data.shape[1] - self.ecc_bytes if length is None else length
         result = np.zeros(ncw, np.int32)
-        _check(lib().ezbch_decode_host(self._h, _np(data), stride, length, _np(ecc),
-                                       ecc.shape[1] if ecc is not None else 0, _np(result),
-                                       _np(errloc), errloc.shape[1] if errloc is not None else 0,
-                                       ncw, chunk), "ezbch_decode_host", True)
+        _check(lib().ezbch_decode_host(self._h, _np(data), ds, length, _np(ecc), es, _np(result),
+                                       _np(errloc), ls, ncw, chunk), "ezbch_decode_host", True)
         return result
 
 

@@ -51,25 +51,31 @@ int ezbch_create_nkt(ezbch_codec **out, unsigned n, unsigned k, unsigned t, int 
 int ezbch_destroy(ezbch_codec *codec);
 int ezbch_get_info(const ezbch_codec *codec, ezbch_info *info);
 
-/* Batch encode -- for every codeword k < ncw: ecc_k = encode_bch(data_k, len) with a zeroed ECC.
- * ecc == NULL: the ECC follows the data in the row (data + len), ecc_stride = data_stride. */
+/* Batch encode -- for every codeword k < ncw: ecc_k = encode_bch(data_k, len) with a zeroed ECC
+ * (bch:196-205).  The data rows are only read; ecc is required (-EINVAL if NULL). */
 int ezbch_encode(const ezbch_codec *codec, const uint8_t *data, size_t data_stride, unsigned len,
                  uint8_t *ecc, size_t ecc_stride, size_t ncw, void *stream);
+/* Row form: each row carries its ECC after its data (rows + len), as in bch:184-195. */
+int ezbch_encode_rows(const ezbch_codec *codec, uint8_t *rows, size_t stride, unsigned len,
+                      size_t ncw, void *stream);
 
 /* Batch decode, in place -- for every codeword k < ncw:
  *   result[k] = correct_bch(data_k, len, ecc_k, errloc_k)
  * i.e. the number of corrected bits (0 for a valid codeword), -74 (EBADMSG) if uncorrectable,
  * -22 (EINVAL) if 8*len > n - ecc_bits; the reported bits are flipped in data and ECC.
  * errloc (nullable): uint32 rows of errloc_stride >= t entries; entries 0..result[k]-1 receive the
- * error locations in ascending order. */
+ * error locations in ascending order.  ecc == NULL: the ECC follows the data in the row. */
 int ezbch_decode(const ezbch_codec *codec, uint8_t *data, size_t data_stride, unsigned len,
                  uint8_t *ecc, size_t ecc_stride, int32_t *result, uint32_t *errloc,
                  size_t errloc_stride, size_t ncw, void *stream);
 
 /* Host-memory forms (blocking), streamed through the device in chunks of `chunk` codewords
- * (0 = library default). */
+ * (0 = library default).  Encode moves only the data bytes in and a compact ECC block out; the
+ * caller's data bytes are never written. */
 int ezbch_encode_host(ezbch_codec *codec, const uint8_t *data, size_t data_stride, unsigned len,
                       uint8_t *ecc, size_t ecc_stride, size_t ncw, size_t chunk);
+int ezbch_encode_rows_host(ezbch_codec *codec, uint8_t *rows, size_t stride, unsigned len,
+                           size_t ncw, size_t chunk);
 int ezbch_decode_host(ezbch_codec *codec, uint8_t *data, size_t data_stride, unsigned len,
                       uint8_t *ecc, size_t ecc_stride, int32_t *result, uint32_t *errloc,
                       size_t errloc_stride, size_t ncw, size_t chunk);

@@ -15,15 +15,21 @@
  *
  * Conventions
  *   - All compute entry points take DEVICE pointers (hipMalloc'd, on the codec's device) and a
- *     hipStream_t passed as void*; they are asynchronous and never allocate or synchronise once the
- *     codec's workspace is reserved (ezrs_reserve), so they can be captured into a hipGraph.
+ *     hipStream_t passed as void*; they are asynchronous and never synchronise.  A codec is const
+ *     after creation and may be shared by threads and streams, like the reference's codec objects
+ *     (rs_base:602-605): each stream gets its own device workspace (grown on demand, never freed
+ *     before ezrs_destroy), so calls on different streams never share scratch memory.  The *_ws
+ *     forms take a caller-owned workspace of ezrs_workspace_bytes() instead (no allocation at all:
+ *     the form to capture into a hipGraph); ezrs_reserve_stream pre-sizes a stream's workspace.
  *     ezrs_*_host take host pointers and run a chunked, double-buffered H2D/kernel/D2H pipeline.
  *   - A codeword's symbols are stored as its datum type: uint8_t for m <= 8, uint16_t for m > 8
  *     (the reference's TYP, rs:75-89).  Strides are in ELEMENTS of the respective array.
  *   - `len` is the number of data (non-parity) symbols per codeword, 1..N-NROOTS; shorter codewords
  *     are shortened codes with implicit leading zeros (rs_base:1302-1304, 1378).
- *   - parity == NULL means the parity of each codeword immediately follows its data, at
- *     data + len in the same row (the reference's decode(data, len+NROOTS) form, rs_base:1183-1186).
+ *   - Encode reads `data` and writes `parity` (encode(data, len, parity), rs_base:868-904); rows that
+ *     carry their own parity after the data (the reference's pair/container forms, rs_base:778-790)
+ *     go through ezrs_encode_rows.  Decode with parity == NULL: the parity follows the data in the
+ *     row, at data + len (the reference's decode(data, len+NROOTS) form, rs_base:1183-1186).
  *   - Symbols narrower than their datum (e.g. RS(31,K) in uint8_t) follow the reference's masked
  *     path: data bits above the symbol are ignored on encode and preserved on decode; a parity datum
  *     with bits above the symbol fails that codeword's decode with -1 (rs_base:1194-1235).
@@ -41,7 +47,7 @@
 extern "C" {
 #endif
 
-#define EZRS_ABI_VERSION 2
+#define EZRS_ABI_VERSION 3
 
 typedef struct ezrs_codec ezrs_codec;
 
@@ -66,7 +72,7 @@ int ezrs_abi_version(void);
 /* Generic codec over GF(2^m): replaces ezpwd::reed_solomon<TYP,SYM,RTS,FCR,PRM,gfpoly<SYM,PLY>,DUAL>
  * (rs_base:702-1719).  Fails with -EINVAL where the reference's constructor would raise:
  * non-primitive poly (rs_base:623-625), nroots == 0 or >= N (rs_base:1254-1256), dual with m != 8
- * (rs_base:1188-1190). */
+ * (rs_base:1188-1190); -ENOTSUP for m > 8 with more than 256 parity symbols (engine limit). */
 int ezrs_create(ezrs_codec **out, unsigned symbol_bits, unsigned poly, unsigned fcr,
                 unsigned prim, unsigned nroots, int dual, int device);
 /* ezpwd::RS<N,K> -- the standard polynomial per N, FCR = 1, PRIM = 1 (rs:74-89). */
@@ -77,15 +83,28 @@ int ezrs_create_ccsds(ezrs_codec **out, unsigned k, int dual, int device);
 int ezrs_destroy(ezrs_codec *codec);
 int ezrs_get_info(const ezrs_codec *codec, ezrs_info *info);
 
-/* Pre-size the codec's device workspace for decode batches of up to `ncw` codewords, so that later
- * ezrs_decode calls of that size neither allocate nor synchronise (graph-capture safe). */
+/* Pre-size the workspace of `stream` (NULL: the null stream) for batches of up to `ncw` codewords,
+ * so that later calls of that size on that stream do not allocate. */
 int ezrs_reserve(ezrs_codec *codec, size_t ncw);
+int ezrs_reserve_stream(const ezrs_codec *codec, size_t ncw, void *stream);
+/* Device workspace bytes a batch of ncw codewords needs (encode and decode alike; may be 0). */
+size_t ezrs_workspace_bytes(const ezrs_codec *codec, size_t ncw);
 
 /* Batch encode -- for every codeword k < ncw:
  *   encode<TYP>(data + k*data_stride, len, parity + k*parity_stride)          rs_base:868-904
- * data and parity are device arrays of the datum type. */
+ * data and parity are device arrays of the datum type; data is only read, parity is required. */
 int ezrs_encode(const ezrs_codec *codec, const void *data, size_t data_stride, unsigned len,
                 void *parity, size_t parity_stride, size_t ncw, void *stream);
+/* Row form: row k holds len data symbols followed by its NROOTS parity symbols (written):
+ *   encode(std::pair(rows_k, rows_k + len + NROOTS))                          rs_base:778-790 */
+int ezrs_encode_rows(const ezrs_codec *codec, void *rows, size_t stride, unsigned len, size_t ncw,
+                     void *stream);
+/* The same with a caller-owned device workspace of >= ezrs_workspace_bytes(codec, ncw) bytes. */
+int ezrs_encode_ws(const ezrs_codec *codec, const void *data, size_t data_stride, unsigned len,
+                   void *parity, size_t parity_stride, size_t ncw, void *ws, size_t ws_bytes,
+                   void *stream);
+int ezrs_encode_rows_ws(const ezrs_codec *codec, void *rows, size_t stride, unsigned len,
+                        size_t ncw, void *ws, size_t ws_bytes, void *stream);
 
 /* Batch decode -- for every codeword k < ncw, in place:
  *   result[k] = decode<TYP>(data + k*data_stride, len, parity + k*parity_stride,
@@ -105,16 +124,25 @@ int ezrs_decode(const ezrs_codec *codec, void *data, size_t data_stride, unsigne
                 void *parity, size_t parity_stride, const uint32_t *eras, size_t eras_stride,
                 const uint32_t *neras, int32_t *result, uint32_t *positions, size_t pos_stride,
                 void *corr, size_t corr_stride, size_t ncw, void *stream);
+int ezrs_decode_ws(const ezrs_codec *codec, void *data, size_t data_stride, unsigned len,
+                   void *parity, size_t parity_stride, const uint32_t *eras, size_t eras_stride,
+                   const uint32_t *neras, int32_t *result, uint32_t *positions, size_t pos_stride,
+                   void *corr, size_t corr_stride, size_t ncw, void *ws, size_t ws_bytes,
+                   void *stream);
 
 /* Host-memory forms: the same contracts with HOST pointers.  The batch is streamed through the
  * device in chunks of `chunk` codewords (0 = library default) over two HIP streams with
- * asynchronous copies; pinned host memory (ezrs_host_alloc) gets full PCIe overlap.  When the
- * parity lies inside the row (parity == NULL, or data + len at the same stride), rows move as
- * one linear copy per chunk each way, and ezrs_encode_host writes each row back whole (its data
- * symbols unchanged).  Blocking:
- * they return when the results are back in host memory. */
+ * asynchronous copies; pinned host memory (ezrs_host_alloc) gets full PCIe overlap.  Blocking:
+ * they return when the results are back in host memory.
+ * Encode sends each chunk's rows to the device (one linear copy of the rows' span when the row
+ * pitch is at most about twice the row; otherwise the rows are gathered into pinned staging first)
+ * and brings back only the parity, as one compact block that is then scattered into place: the
+ * caller's data symbols are never written.  Decode copies inline-parity rows as one linear span
+ * each way. */
 int ezrs_encode_host(ezrs_codec *codec, const void *data, size_t data_stride, unsigned len,
                      void *parity, size_t parity_stride, size_t ncw, size_t chunk);
+int ezrs_encode_rows_host(ezrs_codec *codec, void *rows, size_t stride, unsigned len, size_t ncw,
+                          size_t chunk);
 int ezrs_decode_host(ezrs_codec *codec, void *data, size_t data_stride, unsigned len,
                      void *parity, size_t parity_stride, const uint32_t *eras,
                      size_t eras_stride, const uint32_t *neras, int32_t *result,

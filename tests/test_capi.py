@@ -22,7 +22,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert ezrs.lib().ezrs_abi_version() == 2
+    assert ezrs.lib().ezrs_abi_version() == 3
 
 
 def test_invalid_codecs_rejected_before_device():
@@ -33,12 +33,23 @@ def test_invalid_codecs_rejected_before_device():
     assert L.ezrs_create(C.byref(h), 10, 0x409, 1, 1, 32, 1, 0) == -errno.EINVAL
     assert L.ezrs_create_rs(C.byref(h), 256, 223, 0) == -errno.EINVAL
     assert L.ezrs_create_ccsds(C.byref(h), 224, 1, 0) == -errno.EINVAL
+    # wide symbols: at most 256 parity symbols (engine limit), rejected before any device work
+    assert L.ezrs_create(C.byref(h), 10, 0x409, 1, 1, 257, 0, 0) == -errno.ENOTSUP
+    assert L.ezrs_create_rs(C.byref(h), 65535, 65000, 0) == -errno.ENOTSUP
     assert not h.value
 
 
 def test_null_codec_calls_are_einval():
     L = ezrs.lib()
     assert L.ezrs_encode(None, None, 0, 1, None, 0, 1, None) == -errno.EINVAL
+    assert L.ezrs_encode_rows(None, None, 0, 1, 1, None) == -errno.EINVAL
+    assert L.ezrs_encode_ws(None, None, 0, 1, None, 0, 1, None, 0, None) == -errno.EINVAL
+    assert L.ezrs_decode_ws(None, None, 0, 1, None, 0, None, 0, None, None, None, 0, None, 0, 1,
+                            None, 0, None) == -errno.EINVAL
+    assert L.ezrs_encode_host(None, None, 0, 1, None, 0, 1, 0) == -errno.EINVAL
+    assert L.ezrs_encode_rows_host(None, None, 0, 1, 1, 0) == -errno.EINVAL
+    assert L.ezrs_reserve_stream(None, 1, None) == -errno.EINVAL
+    assert L.ezrs_workspace_bytes(None, 1) == 0
     assert L.ezrs_decode(None, None, 0, 1, None, 0, None, 0, None, None, None, 0, None, 0, 1,
                          None) == -errno.EINVAL
     assert L.ezrs_destroy(None) == 0

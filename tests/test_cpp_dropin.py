@@ -34,7 +34,40 @@ def test_header_builds_and_fails_loudly_without_gpu(tmp_path):
         pytest.skip("a GPU is present; covered by the gpu test")
     p = subprocess.run([exe, "1"], capture_output=True, text=True, timeout=120)
     assert p.returncode == 3, p.stdout + p.stderr
-    assert p.stdout.startswith("NODEV"), p.stdout
+    lines = p.stdout.splitlines()
+    # codec objects construct without a GPU (the GPU codec is created lazily, so a static codec
+    # costs nothing at start-up); the first call fails loudly
+    assert lines[0].startswith("# RS(255,223)"), p.stdout
+    assert lines[1].startswith("NODEV"), p.stdout
+
+
+REF_RSENCODE = "/root/reference/rsencode.C"
+
+
+def build_reference_rsencode(out, extra=()):
+    """Compile the reference's own rsencode.C, UNCHANGED, against this repository's drop-in: the
+    include path puts include/ (whose ezpwd/rs forwards to ezpwd_amd/rs) before the reference's
+    c++/ directory, which still supplies <ezpwd/output>.  Returns the executable path."""
+    cmd = ["g++", "-std=c++17", "-O2", "-Wall", *extra, "-I", os.path.join(ROOT, "include"),
+           "-I", "/root/reference/c++", REF_RSENCODE, "-L", LIBDIR, "-lezrs_hip",
+           f"-Wl,-rpath,{LIBDIR}", "-o", out]
+    subprocess.run(cmd, check=True, capture_output=True, text=True)
+    return out
+
+
+@pytest.mark.skipif(not os.path.exists(REF_RSENCODE), reason="reference tree absent")
+def test_reference_rsencode_builds_unchanged(tmp_path):
+    """rsencode.C:93-163 uses RS_t::symbol_t, rs.NROOTS, rs.SYMBOL and the string / vector
+    encode/decode overloads: it must compile against the drop-in with only the include path
+    switched, for 8- and 16-bit symbols (GNUmakefile's rsencode / rsencode_16)."""
+    if not os.path.exists(os.path.join(LIBDIR, "libezrs_hip.so")):
+        pytest.skip("libezrs_hip.so not built")
+    exe = build_reference_rsencode(str(tmp_path / "rsencode"))
+    build_reference_rsencode(str(tmp_path / "rsencode_16"),
+                             ("-DRSCODEWORD=65535", "-DRSPARITY=64"))
+    if not os.path.exists("/dev/kfd"):
+        p = subprocess.run([exe], input=b"abcd\n", capture_output=True, timeout=60)
+        assert p.returncode == 1 and b"cannot create codec on the GPU" in p.stderr
 
 
 def _parse(line):
