@@ -41,46 +41,55 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(seconds=12.0, threads=None):
-    """Time the reference codec (oracle/_ref, compiled from /root/reference) -- or, if that build
-    is absent, the oracle restatement -- on this host: RS(255,223) encode + clean decode of a
-    bounded sample of the C2 workload, one slice per thread.  Returns the JSON object."""
-    import numpy as np
-    import oracle as O
-    threads = threads or min(16, os.cpu_count() or 1)
-    use_ref = O.Ref.available()
-    if use_ref:
-        idx = O.Ref.index("RS(255,223)")
-        kind = "reference"
-    else:
-        oc = O.Codec(*O.rs_params(N, K))
-        kind = "port"
-    rng = np.random.default_rng(0x5EED0002)
-    per = 4096
-    bufs = [rng.integers(0, 256, (per, N)).astype(np.uint8) for _ in range(threads)]
-    pars = [np.zeros((per, NR), np.uint8) for _ in range(threads)]
+def host_cpu_info():
+    """CPU model, logical CPUs (nproc), the CPUs this process may run on, the cgroup CPU quota
+    and the physical core count of the host."""
+    info = {"model": "?", "nproc": os.cpu_count() or 1}
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    info["model"] = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        info["affinity"] = info["nproc"]
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    info["cgroup_quota"] = quota
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu", "-p=core,socket"], capture_output=True, text=True,
+                             timeout=10).stdout
+        cores = {tuple(l.split(",")[:2]) for l in out.splitlines() if l and not l.startswith("#")}
+        info["physical_cores"] = len(cores) or None
+    except Exception:
+        info["physical_cores"] = None
+    usable = min(x for x in (info["affinity"], quota, info["physical_cores"]) if x)
+    info["threads_used"] = usable
+    return info
 
-    def one(t):
-        b, p = bufs[t], pars[t]
-        if use_ref:
-            O.Ref.encode_batch(idx, b, K, p)
-            b[:, K:] = p
-            O.Ref.decode_batch(idx, b, K, b[:, K:].copy())
-        else:
-            oc.encode_batch(b, K, None)
-            oc.decode_batch(b, K, None)
 
-    # calibrate on one round, then run enough rounds for ~`seconds` of wall time
+def _time_threads(one, threads, seconds):
+    """Run one(t) repeatedly on `threads` threads for about `seconds`; returns (items, dt)."""
     t0 = time.perf_counter()
-    one(0)
+    n0 = one(0)
     per_round = time.perf_counter() - t0
     rounds = max(1, int(seconds / max(per_round, 1e-6)))
     counts = [0] * threads
 
     def worker(t):
         for _ in range(rounds):
-            one(t)
-            counts[t] += per
+            counts[t] += one(t)
 
     ths = [threading.Thread(target=worker, args=(t,)) for t in range(threads)]
     t0 = time.perf_counter()
@@ -88,13 +97,120 @@ def cpu_baseline(seconds=12.0, threads=None):
         th.start()
     for th in ths:
         th.join()
-    dt = time.perf_counter() - t0
-    ncw = sum(counts)
-    return {"value": round(ncw * N / dt / 1e9, 4), "unit": "GB/s", "cores": threads,
-            "kind": kind,
-            "sample": f"RS(255,223) encode+clean decode of {ncw} random codewords "
-                      f"({threads} threads x {rounds} rounds x {per} cw, {dt:.1f} s), "
-                      f"{'reference ezpwd::RS<255,223> (oracle/_ref)' if use_ref else 'oracle restatement'}"}
+    return sum(counts), time.perf_counter() - t0
+
+
+def cpu_baselines(seconds=4.0):
+    """The reference codec (oracle/_ref, compiled from /root/reference; the oracle restatement
+    where that build or codec is absent) timed on this host's cores, single-threaded and on every
+    usable physical core, for the SURVEY 8(d) configs: C2 (the headline), C1, C3, C4 and C5 (BCH:
+    the restatement of the absent Djelic library).  Bounded samples of `seconds` each.  Returns the
+    cpu_baseline object of the C2 line (value = all-core C2 rate) with the other rows attached."""
+    import numpy as np
+    import oracle as O
+    info = host_cpu_info()
+    nth = info["threads_used"]
+    use_ref = O.Ref.available()
+    rng = np.random.default_rng(0x5EED0002)
+
+    def rs_rows(n, k, per, nerr, nera, dtype=np.uint8):
+        """`per` encoded rows + corrupted copies (nerr errors + nera erasures per row)."""
+        nn = n if dtype == np.uint8 else 65535
+        data = rng.integers(0, nn + 1, (per, n)).astype(dtype)
+        oc = O.Codec(*O.rs_params(n, k))
+        oc.encode_batch(data, k, None, nthreads=8)
+        bad = data.copy()
+        eras = np.zeros((per, max(1, n - k)), np.uint32)
+        neras = np.zeros(per, np.uint32)
+        if nerr + nera:
+            for r in range(per):
+                locs = rng.choice(n, nerr + nera, replace=False)
+                bad[r, locs] ^= rng.integers(1, nn + 1, nerr + nera).astype(dtype)
+                eras[r, :nera] = locs[nerr:]
+            neras[:] = nera
+        return data, bad, eras, neras
+
+    def rs_case(name, n, k, per, nerr, nera, encode, dtype=np.uint8):
+        data, bad, eras, neras = rs_rows(n, k, per, nerr, nera, dtype)
+        idx = None
+        if use_ref:
+            try:
+                idx = O.Ref.index(f"RS({n},{k})")
+            except KeyError:
+                idx = None
+        oc = O.Codec(*O.rs_params(n, k))
+        bufs = {}
+
+        def one(t):
+            if t not in bufs:
+                bufs[t] = (data.copy(), bad.copy(), np.zeros((per, n - k), dtype))
+            d, b, p = bufs[t]
+            if nerr + nera:
+                b[:] = bad                    # corrections are in place: restore the input
+            if idx is not None:
+                L = O.Ref.lib()
+                if encode:
+                    L.ezref_encode_batch(idx, d.ctypes.data, n, k,
+                                         p.ctypes.data, n - k, per, d.itemsize)
+                # inline parity: the parity of row r starts at b[r, k] (stride n)
+                L.ezref_decode_batch(idx, b.ctypes.data, n, k, b.ctypes.data + k * b.itemsize, n,
+                                     eras.ctypes.data if nera else None, eras.shape[1],
+                                     neras.ctypes.data if nera else None, res.ctypes.data, None, 0,
+                                     per, b.itemsize)
+            else:
+                if encode:
+                    oc.encode_batch(d, k, p)
+                oc.decode_batch(b, k, None, eras if nera else None, neras if nera else None)
+            return per
+        res = np.zeros(per, np.int32)
+        row = {"workload": name, "kind": "reference" if idx is not None else "port"}
+        for label, th in (("threads_1", 1), ("threads_all", nth)):
+            ncw, dt = _time_threads(one, th, seconds)
+            row[label] = round(ncw * n * np.dtype(dtype).itemsize / dt / 1e9, 5)
+            row[label + "_sample"] = f"{ncw} codewords in {dt:.2f} s"
+        return row
+
+    rows = {
+        "C2": rs_case("RS(255,223) encode + clean decode", 255, 223, 4096, 0, 0, True),
+        "C1": rs_case("RS(255,251) encode + decode, 1 error per codeword", 255, 251, 10000, 1, 0,
+                      True),
+        "C3": rs_case("RS(255,223) decode, 8 errors + 4 erasures", 255, 223, 2048, 8, 4, False),
+        "C4": rs_case("RS(65535,65503) encode + decode, 8 errors + 4 erasures", 65535, 65503, 16,
+                      8, 4, True, np.uint16),
+    }
+    # C5: BCH(1023,983,4), 122 data + 5 ECC bytes, 0..4 bit errors (restatement: Djelic is absent)
+    b = O.BCH(10, 4)
+    per = 20000
+    d = rng.integers(0, 256, (per, 127)).astype(np.uint8)
+    b.encode_batch(d, 122, None, nthreads=8)
+    bad = d.copy()
+    cnt = rng.integers(0, 5, per)
+    for r in range(per):
+        for p in rng.choice(8 * 127, int(cnt[r]), replace=False):
+            bad[r, p // 8] ^= np.uint8(0x80 >> (p % 8))
+    bb = {}
+
+    def one5(t):
+        if t not in bb:
+            bb[t] = (d.copy(), bad.copy())
+        x, y = bb[t]
+        b.encode_batch(x, 122, None)
+        y[:] = bad
+        b.decode_batch(y, 122, None)
+        return per
+    c5 = {"workload": "BCH(1023,983,4) encode + decode, 0-4 bit errors", "kind": "port"}
+    for label, th in (("threads_1", 1), ("threads_all", nth)):
+        ncw, dt = _time_threads(one5, th, seconds)
+        c5[label] = round(ncw * 127 / dt / 1e9, 5)
+        c5[label + "_sample"] = f"{ncw} codewords in {dt:.2f} s"
+    rows["C5"] = c5
+    c2 = rows["C2"]
+    return {"value": c2["threads_all"], "unit": "GB/s", "cores": nth, "kind": c2["kind"],
+            "sample": f"RS(255,223) encode+clean decode, {c2['threads_all_sample']} on {nth} "
+                      f"threads ({'reference ezpwd::RS<255,223>, oracle/_ref' if c2['kind'] == 'reference' else 'oracle restatement'})",
+            "single_thread": c2["threads_1"], "cpu_model": info["model"], "nproc": info["nproc"],
+            "affinity_cpus": info["affinity"], "cgroup_quota": info["cgroup_quota"],
+            "physical_cores": info["physical_cores"], "rows": rows}
 
 
 def load_traffic(kernel_call):
@@ -294,6 +410,63 @@ def bench_c5(args):
         dist.destroy_process_group()
 
 
+def relaunch_distributed(args):
+    """`bench.py --gpus N` started directly (not under torchrun): run N ranks, one process per GPU,
+    through torch.distributed.run on this node, and return its exit status.  Nothing here touches
+    the GPU before the ranks are started."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1", "--master-port",
+           str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    log(f"bench: launching {args.gpus} ranks: {' '.join(cmd)}")
+    return subprocess.call(cmd, env=env)
+
+
+def harness_check(args):
+    """The multi-rank harness alone, on CPU with gloo (tests/test_bench_harness.py): the same
+    launch, barrier + max-over-ranks timing and JSON line as the GPU workloads, with a placeholder
+    step (an XOR pass over a host buffer, no codec work).  Never a measurement."""
+    import numpy as np
+    import torch.distributed as dist
+    import shard
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    lo, hi = shard.shard_range(args.ncw * world, world, rank)
+    buf = np.random.default_rng(rank).integers(0, 256, (hi - lo, 255), dtype=np.uint8)
+    acc = np.zeros(255, np.uint8)
+    for _ in range(args.warmup):
+        np.bitwise_xor.reduce(buf, axis=0, out=acc)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        np.bitwise_xor.reduce(buf, axis=0, out=acc)
+    if world > 1:
+        dist.barrier()
+    t = shard.max_over_ranks(time.perf_counter() - t0)
+    counts = shard.sum_over_ranks([hi - lo])
+    if rank == 0:
+        print(json.dumps({"metric": "harness check (no codec work)", "value": None, "unit": None,
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(t / args.steps * 1e3, 4),
+                          "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                          "dtype": "u8", "data": "harness check: placeholder step, gloo, CPU",
+                          "config": {"workload": "harness", "codewords_total": counts[0],
+                                     "parallelism": f"shard{world}"},
+                          "roofline": None, "cpu_baseline": None}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -301,12 +474,21 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--ncw", type=int, default=1 << 20, help="codewords per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=3.0,
+                    help="seconds per CPU-baseline measurement (5 configs x 1/all threads)")
     ap.add_argument("--e2e", action="store_true", help="also time the host-memory pipeline")
     ap.add_argument("--workload", choices=("c2", "c3", "c4", "c5"), default="c2",
                     help="c2: the headline RS(255,223) line; c3: RS(255,223) 8 errors + 4 erasures "
                          "decode; c4: RS(65535,65503); c5: BCH(1023,983,4) (SURVEY.md 8d)")
+    ap.add_argument("--harness-check", action="store_true",
+                    help="CPU/gloo check of the multi-rank harness (placeholder step, no GPU)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch_distributed(args))
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
+        log(f"bench: note: WORLD_SIZE={os.environ['WORLD_SIZE']} ranks, --gpus {args.gpus}")
+    if args.harness_check:
+        return harness_check(args)
     if args.workload == "c5":
         return bench_c5(args)
     if args.workload in ("c3", "c4"):
@@ -399,7 +581,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_seconds)
+        cpu = cpu_baselines(args.cpu_seconds)
 
     if rank == 0:
         line = {"metric": "RS(255,223) encode+decode GB/s device-resident",

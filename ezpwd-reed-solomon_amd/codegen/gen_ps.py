@@ -1,0 +1,368 @@
+#!/usr/bin/env python3
+"""Generate the plane-sliced GF(2^8) RS syndrome kernels' constant code (csrc/gen/ezrs_ps_tables.inc).
+
+Word layout.  A 32-bit word holds ONE position of FOUR codewords: byte k = the symbol of codeword
+k, so bit 8k + b is bit-plane b of codeword k.  Every bit of the word is an independent GF(2)
+stream (codeword k, plane b); the kernels never separate the planes of a symbol.
+
+Plane slicing.  With r_p = sum_b bit_b(r_p) alpha^b (polynomial basis), a syndrome is
+
+    S_e = r(alpha^e) = sum_b alpha^b V_{b,e},     V_{b,e} = sum_p bit_b(r_p) w_e(p),
+    w_e(p) = alpha^(e (N-1-p))                          (c++/ezpwd/rs_base:1390-1414)
+
+and, because the V's coefficients are bits, V_{b,2e} = V_{b,e}^2.  So only one root per
+cyclotomic coset ("leader") is evaluated in the main loop -- 16 of the 32 roots of RS(255,223) --
+and the others follow by squaring in the epilogue: the main loop's state is 8 GF(2^8) bits per
+leader, 128 words for RS(255,223), half of what a per-symbol bit-slicing of 32 syndromes needs.
+
+Main loop.  Per 8 positions and leader bit q the state word takes one 3-input XOR of two
+Four-Russians combinations (all 15 XORs of four position words are formed once per 4 positions).
+A workgroup of 8 waves covers a tile of 256 codewords (4 per lane): wave (g, q) evaluates leader
+group g (8 leaders) over position slice q (S positions).  All slices run the SAME code (slice 0's
+weights); slice q's partials are then multiplied by alpha^(-q S e) ("fixup").
+
+Epilogue (after the partials are summed across slices): expansion (squarings) and the plane fold
+S = sum_b alpha^b V_b inside each byte (3 levels: x alpha, x alpha^2, x alpha^4 with shifts 1,2,4),
+four syndromes packed per word in the upper levels.  Output: "quads" of 8 words whose bit 8k + j
+is bit q of syndrome j of the quad for codeword k.
+
+Encode: syndromes of the data symbols (positions 0..K-1 of the full frame) go to a workspace; the
+parity kernel maps them to parity with the GF(2) matrix of  parity = V^-1 S  (V_{e,j} =
+alpha^(e (NR-1-j))), applied bit-sliced over 32 codewords per lane (q_pass, same as gen_bitslice).
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+from gf8 import GF8, gf_mat_inv, lin_rows  # noqa: E402
+
+N = 255
+WAVES = 8                 # waves per workgroup (tile of 256 codewords)
+NLG = 8                   # leader slots per group (state = 8 * NLG words per wave)
+S_DEC = 64                # positions per slice: decode covers 256 (4 x 64); encode 4 x S_ENC >= K
+
+# (name, poly, fcr, prim, nroots): codecs with a plane-sliced path (leaders <= 16)
+CODECS = [
+    ("RS_255_223", 0x11d, 1, 1, 32),
+    ("RS_255_239", 0x11d, 1, 1, 16),
+    ("RS_255_251", 0x11d, 1, 1, 4),
+]
+
+
+def fmt_list(xs):
+    return "{" + ", ".join(str(x) for x in xs) + "}"
+
+
+class PsCodec:
+    def __init__(self, name, poly, fcr, prim, nr):
+        self.name, self.poly, self.fcr, self.prim, self.nr = name, poly, fcr, prim, nr
+        gf = self.gf = GF8(poly)
+        self.exps = [((fcr + i) * prim) % N for i in range(nr)]   # syndrome i <-> alpha^exps[i]
+        # cyclotomic cosets: leader = first syndrome index of each coset hit by the roots
+        leaders, members = [], {}
+        for i, e in enumerate(self.exps):
+            for l in leaders:
+                el, k, x = self.exps[l], 0, self.exps[l]
+                found = None
+                for k in range(8):
+                    if x == e:
+                        found = k
+                        break
+                    x = (2 * x) % N
+                if found is not None:
+                    members[l].append((i, found))
+                    break
+            else:
+                leaders.append(i)
+                members[i] = [(i, 0)]
+        self.leaders, self.members = leaders, members
+        L = len(leaders)
+        assert L <= 16, "plane-sliced path supports at most 16 leaders"
+        self.R = 2
+        self.PI = WAVES // self.R
+        # encode slices: 4 x s_enc >= K data positions, a multiple of 8 (blocks of 8 positions)
+        self.s_enc = 8 * -(-(N - nr) // 32)
+        # assign leaders to (group, slot); final owner of slots {2i, 2i+1} of group g is the wave
+        # with idx(q) = 2 (q & 1) + (q >> 1) == i  (see the reduction in ezrs_ps.hip).  Pair big
+        # families with small ones so that every wave folds a similar number of syndromes.
+        order = sorted(leaders, key=lambda l: -len(members[l]))
+        pairs = []
+        lo, hi = 0, len(order) - 1
+        while lo <= hi:
+            if lo == hi:
+                pairs.append((order[lo], None))
+            else:
+                pairs.append((order[lo], order[hi]))
+            lo += 1
+            hi -= 1
+        while len(pairs) < 8:
+            pairs.append((None, None))
+        pairs.sort(key=lambda p: -sum(len(members[x]) for x in p if x is not None))
+        # spread the 8 pairs over (g, i): pair rank r -> g = r & 1, i = r >> 1
+        self.slot = {}            # leader -> (g, slot)
+        self.group = [[None] * NLG for _ in range(self.R)]
+        for r, (a, b) in enumerate(pairs):
+            g, i = r & 1, r >> 1
+            for s, l in ((2 * i, a), (2 * i + 1, b)):
+                self.group[g][s] = l
+                if l is not None:
+                    self.slot[l] = (g, s)
+        # epilogue: wave (g, q) folds the syndromes of the two leaders it owns
+        self.epi = {}
+        for g in range(self.R):
+            for i in range(4):
+                syn = []
+                for s in (2 * i, 2 * i + 1):
+                    l = self.group[g][s]
+                    if l is not None:
+                        syn += [(s - 2 * i, m, k) for m, k in members[l]]
+                self.epi[(g, i)] = syn   # (local leader 0/1, syndrome index, squarings)
+        self.nq = max((len(v) + 3) // 4 for v in self.epi.values())
+        # parity map: p = Vinv S  (S with the x^NR factor included)
+        V = [[gf.pow_alpha(e * (nr - 1 - j)) for j in range(nr)] for e in self.exps]
+        self.Vinv = gf_mat_inv(gf, V)
+
+    # weight of full-frame position p for syndrome i
+    def w(self, i, p):
+        return self.gf.pow_alpha(self.exps[i] * (N - 1 - p))
+
+    def q_rows(self):
+        """8 NR rows (parity symbol j, bit b) as masks over input bits 8 i + q (syndrome i, bit q)."""
+        gf, nr = self.gf, self.nr
+        rows = []
+        for j in range(nr):
+            for b in range(8):
+                m = 0
+                for i in range(nr):
+                    for q in range(8):
+                        if gf.mul(self.Vinv[j][i], 1 << q) >> b & 1:
+                            m |= 1 << (8 * i + q)
+                rows.append(m)
+        return rows
+
+
+def xor_chain(dst, terms, ind):
+    """dst = XOR of terms, folded left with v_bitop3 three-input XORs."""
+    if not terms:
+        return [f"{ind}{dst} = 0u;"]
+    acc, rest = terms[0], terms[1:]
+    while rest:
+        if len(rest) >= 2:
+            acc, rest = f"xor3({acc}, {rest[0]}, {rest[1]})", rest[2:]
+        else:
+            acc, rest = f"({acc} ^ {rest[0]})", rest[1:]
+    return [f"{ind}{dst} = {acc};"]
+
+
+def emit_combos(out, name, srcs, ind):
+    a = srcs
+    out.append(f"{ind}const uint32_t {name}1 = {a[0]}, {name}2 = {a[1]}, {name}4 = {a[2]}, {name}8 = {a[3]};")
+    out.append(f"{ind}const uint32_t {name}3 = {name}1 ^ {name}2, {name}5 = {name}1 ^ {name}4, "
+               f"{name}6 = {name}2 ^ {name}4, {name}9 = {name}1 ^ {name}8, {name}10 = {name}2 ^ {name}8, "
+               f"{name}12 = {name}4 ^ {name}8;")
+    out.append(f"{ind}const uint32_t {name}7 = {name}3 ^ {name}4, {name}11 = {name}3 ^ {name}8, "
+               f"{name}13 = {name}5 ^ {name}8, {name}14 = {name}6 ^ {name}8;")
+    out.append(f"{ind}const uint32_t {name}15 = {name}7 ^ {name}8;")
+    out.append(f"{ind}(void){name}1; (void){name}2; (void){name}3; (void){name}4; (void){name}5; "
+               f"(void){name}6; (void){name}7; (void){name}8; (void){name}9; (void){name}10; "
+               f"(void){name}11; (void){name}12; (void){name}13; (void){name}14; (void){name}15;")
+
+
+def mat_apply(out, dst, src, rows, ind, extra=None):
+    """dst[q] = (extra[q] ^) XOR over b in rows[q] of src[b]; src and dst distinct arrays."""
+    for q in range(8):
+        terms = ([extra[q]] if extra else []) + [src[b] for b in range(8) if rows[q] >> b & 1]
+        out.extend(xor_chain(dst[q], terms, ind))
+
+
+def gen_codec(c: PsCodec):
+    gf = c.gf
+    st = f"PS_{c.name}"
+    out = [f"struct {st} {{",
+           f"    static constexpr unsigned POLY = {c.poly:#x}, FCR = {c.fcr}, PRIM = {c.prim}, NR = {c.nr};",
+           f"    static constexpr int R = {c.R}, PI = {c.PI}, NLG = {NLG}, NQ = {c.nq};",
+           f"    static constexpr int S_DEC = {S_DEC}, S_ENC = {c.s_enc};",
+           "    // main loop: positions 8B..8B+7 of slice 0 (words X[0..7]) into group G's state",
+           "    template <int G, int B> static __device__ void block(uint32_t (&V)[NLG][8], const uint32_t (&X)[8]);",
+           "    // slice-q partials of group G times alpha^(-q S e) (S = S_DEC or S_ENC)",
+           "    template <int G, int S> static __device__ void fixup(uint32_t (&V)[NLG][8], int q);",
+           "    // wave (G, I) epilogue: the totals of its two leaders -> NQ quads of syndromes",
+           "    template <int G, int I> static __device__ void epilogue(const uint32_t (&T)[2][8], uint32_t (&Q)[NQ][8]);",
+           "    // syndrome index of quad slot (wave (G, I), quad, j), -1 = none",
+           f"    static constexpr int SYN[{c.R}][4][{c.nq}][4] = " + "{" + ", ".join(
+               "{" + ", ".join("{" + ", ".join(
+                   "{" + ", ".join(str(c.epi[(g, i)][4 * qd + j][1]) if 4 * qd + j < len(c.epi[(g, i)]) else "-1"
+                                   for j in range(4)) + "}" for qd in range(c.nq)) + "}"
+                   for i in range(4)) + "}" for g in range(c.R)) + "};",
+           "    template <int P> static __device__ void q_pass(uint32_t (&O)[8][8], const uint32_t *in, int ld);",
+           f"    static constexpr int NPASS = {(c.nr + 7) // 8};",
+           "};"]
+    I = "    "
+    # ---- main-loop blocks
+    for g in range(c.R):
+        for B in range(S_DEC // 8):
+            out.append(f"template <> __device__ __forceinline__ void {st}::block<{g}, {B}>("
+                       "uint32_t (&V)[NLG][8], const uint32_t (&X)[8]) {")
+            emit_combos(out, "l", [f"X[{t}]" for t in range(4)], I)
+            emit_combos(out, "h", [f"X[{t}]" for t in range(4, 8)], I)
+            for s in range(NLG):
+                l = c.group[g][s]
+                if l is None:
+                    continue
+                for q in range(8):
+                    m1 = sum(((c.w(l, 8 * B + t) >> q) & 1) << t for t in range(4))
+                    m2 = sum(((c.w(l, 8 * B + 4 + t) >> q) & 1) << t for t in range(4))
+                    terms = ([f"l{m1}"] if m1 else []) + ([f"h{m2}"] if m2 else [])
+                    if len(terms) == 2:
+                        out.append(f"{I}V[{s}][{q}] = xor3(V[{s}][{q}], {terms[0]}, {terms[1]});")
+                    elif terms:
+                        out.append(f"{I}V[{s}][{q}] ^= {terms[0]};")
+            out.append("}")
+    # ---- fixups
+    for g in range(c.R):
+        for S in sorted({S_DEC, c.s_enc}):
+            out.append(f"template <> __device__ __forceinline__ void {st}::fixup<{g}, {S}>("
+                       "uint32_t (&V)[NLG][8], int q) {")
+            out.append(f"{I}uint32_t t[8];")
+            out.append(f"{I}switch (q) {{")
+            for qq in range(1, c.PI):
+                out.append(f"{I}case {qq}:")
+                for s in range(NLG):
+                    l = c.group[g][s]
+                    if l is None:
+                        continue
+                    cst = gf.pow_alpha((-qq * S * c.exps[l]) % N)
+                    rows = lin_rows(lambda x, cst=cst: gf.mul(cst, x))
+                    out.append(f"{I}    for (int b = 0; b < 8; ++b) t[b] = V[{s}][b];")
+                    mat_apply(out, [f"V[{s}][{q}]" for q in range(8)], [f"t[{b}]" for b in range(8)], rows, I + "    ")
+                out.append(f"{I}    break;")
+            out.append(f"{I}default: break;")
+            out.append(f"{I}}}")
+            out.append("}")
+    # ---- epilogues
+    sq_rows = {}
+
+    def sqk_rows(k):
+        if k not in sq_rows:
+            sq_rows[k] = lin_rows(lambda x, k=k: gf.pow(x, 1 << k) if x else 0)
+        return sq_rows[k]
+
+    a1 = lin_rows(lambda x: gf.mul(2, x))
+    a2 = lin_rows(lambda x: gf.mul(4, x))
+    a4 = lin_rows(lambda x: gf.mul(16, x))
+
+    def fold_level(out, dst, src, rows, sh, ind):
+        # dst[q] = src[q] ^ (alpha-matrix applied to (src >> sh))[q]
+        out.append(f"{ind}{{")
+        out.append(f"{ind}    uint32_t y[8];")
+        out.append(f"{ind}    for (int b = 0; b < 8; ++b) y[b] = {src}[b] >> {sh};")
+        mat_apply(out, [f"{dst}[{q}]" for q in range(8)], [f"y[{b}]" for b in range(8)], rows, ind + "    ",
+                  extra=[f"{src}[{q}]" for q in range(8)])
+        out.append(f"{ind}}}")
+
+    for g in range(c.R):
+        for i in range(4):
+            syn = c.epi[(g, i)]
+            out.append(f"template <> __device__ __forceinline__ void {st}::epilogue<{g}, {i}>("
+                       "const uint32_t (&T)[2][8], uint32_t (&Q)[NQ][8]) {")
+            for qd in range(c.nq):
+                part = syn[4 * qd:4 * qd + 4]
+                out.append(f"{I}{{ // quad {qd}: syndromes {[m for _, m, _ in part]}")
+                # level 1 per syndrome
+                for j in range(4):
+                    out.append(f"{I}    uint32_t F{j}[8];")
+                    if j < len(part):
+                        ll, m, k = part[j]
+                        if k == 0:
+                            out.append(f"{I}    const uint32_t *W{j} = T[{ll}];")
+                        else:
+                            out.append(f"{I}    uint32_t W{j}[8];")
+                            mat_apply(out, [f"W{j}[{q}]" for q in range(8)], [f"T[{ll}][{b}]" for b in range(8)],
+                                      sqk_rows(k), I + "    ")
+                        fold_level(out, f"F{j}", f"W{j}", a1, 1, I + "    ")
+                    else:
+                        out.append(f"{I}    for (int b = 0; b < 8; ++b) F{j}[b] = 0u;")
+                # pack pairs, level 2
+                for pj in range(2):
+                    out.append(f"{I}    uint32_t P{pj}[8], G{pj}[8];")
+                    out.append(f"{I}    for (int b = 0; b < 8; ++b) P{pj}[b] = bfi(0x55555555u, "
+                               f"F{2 * pj}[b], F{2 * pj + 1}[b] << 1);")
+                    fold_level(out, f"G{pj}", f"P{pj}", a2, 2, I + "    ")
+                out.append(f"{I}    uint32_t H[8];")
+                out.append(f"{I}    for (int b = 0; b < 8; ++b) H[b] = bfi(0x33333333u, "
+                           f"G0[b], G1[b] << 2);")
+                fold_level(out, f"Q[{qd}]", "H", a4, 4, I + "    ")
+                out.append(f"{I}}}")
+            out.append("}")
+    # ---- parity map passes (8 parity symbols each) over 32-codeword bit-sliced syndromes
+    Q = c.q_rows()
+    nr = c.nr
+    for P in range((nr + 7) // 8):
+        j0, nj = 8 * P, min(8, nr - 8 * P)
+        out.append(f"template <> __device__ __forceinline__ void {st}::q_pass<{P}>("
+                   "uint32_t (&O)[8][8], const uint32_t *in, int ld) {")
+        first = [[True] * 8 for _ in range(nj)]
+        out.append(f"{I}uint32_t N[8];")
+        out.append(f"{I}#pragma unroll")
+        out.append(f"{I}for (int q = 0; q < 8; ++q) N[q] = in[q * ld];")
+        for i in range(nr):
+            out.append(f"{I}{{ // syndrome {i}")
+            out.append(f"{I}    uint32_t P[8];")
+            out.append(f"{I}    #pragma unroll")
+            out.append(f"{I}    for (int q = 0; q < 8; ++q) P[q] = N[q];")
+            if i + 1 < nr:
+                out.append(f"{I}    #pragma unroll")
+                out.append(f"{I}    for (int q = 0; q < 8; ++q) N[q] = in[({8 * (i + 1)} + q) * ld];")
+            out.append(f"{I}    __builtin_amdgcn_sched_barrier(0);")
+            emit_combos(out, "l", ["P[0]", "P[1]", "P[2]", "P[3]"], I + "    ")
+            emit_combos(out, "h", ["P[4]", "P[5]", "P[6]", "P[7]"], I + "    ")
+            for jl in range(nj):
+                for b in range(8):
+                    row = Q[8 * (j0 + jl) + b]
+                    m = (row >> (8 * i)) & 0xFF
+                    ml, mh = m & 15, m >> 4
+                    terms = ([f"l{ml}"] if ml else []) + ([f"h{mh}"] if mh else [])
+                    dst = f"O[{jl}][{b}]"
+                    if first[jl][b]:
+                        out.append(f"{I}    {dst} = " + (" ^ ".join(terms) if terms else "0u") + ";")
+                        first[jl][b] = False
+                    elif len(terms) == 2:
+                        out.append(f"{I}    {dst} = xor3({dst}, {terms[0]}, {terms[1]});")
+                    elif terms:
+                        out.append(f"{I}    {dst} ^= {terms[0]};")
+            out.append(f"{I}    __builtin_amdgcn_sched_barrier(0);")
+            out.append(f"{I}}}")
+        out.append("}")
+    return "\n".join(out)
+
+
+def main(dst=None):
+    dst = dst or os.path.join(HERE, "..", "csrc", "gen", "ezrs_ps_tables.inc")
+    os.makedirs(os.path.dirname(dst), exist_ok=True)
+    body = ["// GENERATED by codegen/gen_ps.py -- do not edit.",
+            "// Plane-sliced GF(2^8) RS syndrome kernels' straight-line code (see ezrs_ps.hip).",
+            "#pragma once", "#include <cstdint>", "namespace ezrs { namespace ps {",
+            "__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {",
+            "    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);", "}",
+            "// (m & a) | (~m & b): v_bfi_b32",
+            "__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {",
+            "    return (m & a) | (~m & b);", "}"]
+    for cd in CODECS:
+        body.append(gen_codec(PsCodec(*cd)))
+    body.append("#define EZRS_PS_CODEC_LIST(X) \\")
+    for i, cd in enumerate(CODECS):
+        sep = " \\" if i + 1 < len(CODECS) else ""
+        body.append(f"    X(PS_{cd[0]}){sep}")
+    body.append("} } // namespace ezrs::ps")
+    txt = "\n".join(body) + "\n"
+    old = open(dst).read() if os.path.exists(dst) else None
+    if old != txt:
+        with open(dst, "w") as f:
+            f.write(txt)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else None)

@@ -6,6 +6,7 @@
 // (rs_base:868-904, 1170-1242) and dispatch to the fastest kernel that is bit-exact for the codec:
 // the bit-sliced GF(2^8) kernels where they apply, the generic per-codeword kernels otherwise.
 #include <cerrno>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -31,6 +32,7 @@ struct ezrs_codec {
     size_t hstage_bytes = 0;      // pinned host bytes of each h_stage buffer
     hipStream_t streams[2] = {nullptr, nullptr};
     int bs_id = -1;               // bit-sliced GF(2^8) kernel set, -1 if none
+    int ps_id = -1;               // plane-sliced GF(2^8) kernel set, -1 if none
     // Device workspaces of the batch entry points, one per HIP stream: calls on different streams
     // never share scratch memory, calls on one stream are ordered by the stream.  A workspace only
     // grows; the buffer it replaces is kept until ezrs_destroy, so work already queued (or a
@@ -154,6 +156,9 @@ int ezrs_create(ezrs_codec **out, unsigned symbol_bits, unsigned poly, unsigned 
     if (hipDeviceGetAttribute(&d.ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
         d.ncu = 0;
     c->bs_id = bitslice_codec_id(d);
+    // EZRS_NO_PLANESLICE=1 keeps the per-symbol bit-sliced kernels (A/B measurements)
+    const char *nops = getenv("EZRS_NO_PLANESLICE");
+    c->ps_id = (nops && *nops == '1') ? -1 : planeslice_codec_id(d);
     *out = c;
     return 0;
 }
@@ -214,7 +219,10 @@ namespace {
 
 // Device scratch bytes one batch call of ncw codewords needs (encode and decode alike).
 size_t ws_bytes_for(const ezrs_codec *c, size_t ncw) {
-    return c->bs_id >= 0 ? bs_encode_ws_bytes(ncw) : 0;   // >= ncw * 32 (decode's need)
+    size_t b = 0;                                          // both >= ncw * 32 (decode's need)
+    if (c->bs_id >= 0) b = bs_encode_ws_bytes(ncw);
+    if (c->ps_id >= 0 && ps_ws_bytes(ncw) > b) b = ps_ws_bytes(ncw);
+    return b;
 }
 
 // The calling stream's workspace, grown to at least `bytes` (see ezrs_codec::Ws).
@@ -242,6 +250,7 @@ namespace {
 // The one place that picks kernels: every entry point (device or host-memory) goes through these.
 // ws: bs_encode_ws_bytes(ncw) bytes (bit-sliced path only).
 hipError_t dispatch_encode(const ezrs_codec *c, const EncodeArgs &a, void *ws, hipStream_t st) {
+    if (c->ps_id >= 0 && ps_can_encode(c->dev, a)) return launch_ps_encode(c->ps_id, c->dev, a, ws, st);
     return c->bs_id >= 0 ? launch_bs_encode(c->bs_id, c->dev, a, ws, st) : launch_encode_generic(c->dev, a, st);
 }
 
@@ -251,6 +260,11 @@ hipError_t dispatch_decode(const ezrs_codec *c, const DecodeArgs &a, uint8_t *sy
     const unsigned w = c->dev.mm <= 8 ? 1 : 2;
     const bool contiguous = a.parity == static_cast<char *>(a.data) + (size_t)a.len * w &&
                             a.parity_stride == a.data_stride;
+    if (c->ps_id >= 0 && ps_can_decode(c->dev, a)) {
+        hipError_t e = launch_ps_syndromes(c->ps_id, c->dev, a, syn_ws, st);
+        if (e == hipSuccess) e = launch_decode_flagged(c->dev, a, syn_ws, st);
+        return e;
+    }
     if (c->bs_id >= 0 && contiguous) {
         // Bit-sliced syndromes for the whole batch; the reference algorithm only for the codewords
         // that are not valid as received (or carry erasures to validate).

@@ -77,4 +77,14 @@ hipError_t launch_bs_encode(int id, const DevCodec &d, const EncodeArgs &a, void
 hipError_t launch_bs_syndromes(int id, const DevCodec &d, const DecodeArgs &a, uint8_t *syn_ws,
                                hipStream_t s);
 
+// Plane-sliced GF(2^8) kernels (ezrs_ps.hip) for the codecs of gen/ezrs_ps_tables.inc: row pitch
+// <= 256 bytes; decode needs the parity inside the row.
+int planeslice_codec_id(const DevCodec &d);   // -1 if the codec has no plane-sliced path
+size_t ps_ws_bytes(size_t ncw);
+bool ps_can_encode(const DevCodec &d, const EncodeArgs &a);
+bool ps_can_decode(const DevCodec &d, const DecodeArgs &a);
+hipError_t launch_ps_encode(int id, const DevCodec &d, const EncodeArgs &a, void *ws, hipStream_t s);
+hipError_t launch_ps_syndromes(int id, const DevCodec &d, const DecodeArgs &a, uint8_t *syn_ws,
+                               hipStream_t s);
+
 } // namespace ezrs

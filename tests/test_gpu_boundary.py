@@ -111,7 +111,8 @@ def test_encode_host_reads_only(torch, pitch):
     np.testing.assert_array_equal(rows, before)
     exp = before[:, :255].copy()
     oc.encode_batch(exp, 223)
-    np.testing.assert_array_equal(par, exp[:, 223:])
+    badrows = np.nonzero((par != exp[:, 223:]).any(axis=1))[0]
+    assert len(badrows) == 0, (badrows[:16], [np.nonzero(par[r] != exp[r, 223:])[0] for r in badrows[:4]])
     # parity scattered into a strided array (row pitch 40) lands in place, the rest untouched
     par2 = np.full((ncw, 40), 0xEE, np.uint8)
     c.encode_host(rows, 223, par2, chunk=777)
