@@ -339,6 +339,235 @@ def gen_codec(c: PsCodec):
     return "\n".join(out)
 
 
+def gen_pw(c: PsCodec):
+    """Per-wave variant: one wave owns 256 codewords and ALL leaders (state NL x 8 words), walks every
+    position itself (no slices, no fixups, no cross-wave reduction) and folds all NR syndromes."""
+    gf = c.gf
+    st = f"PW_{c.name}"
+    L = len(c.leaders)
+    # epilogue order: leaders by family size (largest first), members by squaring count, so a
+    # leader's state dies as soon as its family is folded
+    seq = []
+    for li, l in sorted(enumerate(c.leaders), key=lambda x: -len(c.members[x[1]])):
+        for m, k in sorted(c.members[l], key=lambda x: x[1]):
+            seq.append((li, m, k))
+    nq = (len(seq) + 3) // 4
+    syn = [[seq[4 * qd + j][1] if 4 * qd + j < len(seq) else -1 for j in range(4)] for qd in range(nq)]
+    out = [f"struct {st} {{",
+           f"    static constexpr unsigned POLY = {c.poly:#x}, FCR = {c.fcr}, PRIM = {c.prim}, NR = {c.nr};",
+           f"    static constexpr int NL = {L}, NQ = {nq};",
+           "    // positions 8B..8B+7 of the full frame (words X[0..7]) into the state",
+           "    template <int B> static __device__ void block(uint32_t (&V)[NL][8], const uint32_t (&X)[8]);",
+           "    // all syndromes, four per quad; emit(integral_constant<qd>, Q[8]) per quad",
+           "    template <class F> static __device__ void epilogue(const uint32_t (&V)[NL][8], F &&emit);",
+           f"    static constexpr int SYN[{nq}][4] = " + "{" + ", ".join(
+               "{" + ", ".join(str(x) for x in row) + "}" for row in syn) + "};",
+           "};"]
+    I = "    "
+    for B in range(32):
+        out.append(f"template <> __device__ __forceinline__ void {st}::block<{B}>("
+                   "uint32_t (&V)[NL][8], const uint32_t (&X)[8]) {")
+        emit_combos(out, "l", [f"X[{t}]" for t in range(4)], I)
+        emit_combos(out, "h", [f"X[{t}]" for t in range(4, 8)], I)
+        for s, l in enumerate(c.leaders):
+            for q in range(8):
+                m1 = sum(((c.w(l, 8 * B + t) >> q) & 1) << t for t in range(4))
+                m2 = sum(((c.w(l, 8 * B + 4 + t) >> q) & 1) << t for t in range(4))
+                terms = ([f"l{m1}"] if m1 else []) + ([f"h{m2}"] if m2 else [])
+                if len(terms) == 2:
+                    out.append(f"{I}V[{s}][{q}] = xor3(V[{s}][{q}], {terms[0]}, {terms[1]});")
+                elif terms:
+                    out.append(f"{I}V[{s}][{q}] ^= {terms[0]};")
+        out.append("}")
+
+    sq_cache = {}
+
+    def sqk(k):
+        if k not in sq_cache:
+            sq_cache[k] = lin_rows(lambda x, k=k: gf.pow(x, 1 << k) if x else 0)
+        return sq_cache[k]
+
+    def cost(rows):
+        return sum(max(0, bin(r).count("1") - 1) for r in rows)
+
+    a1 = lin_rows(lambda x: gf.mul(2, x))
+    a2 = lin_rows(lambda x: gf.mul(4, x))
+    a4 = lin_rows(lambda x: gf.mul(16, x))
+
+    def fold_level(dst, src, rows, sh, ind):
+        out.append(f"{ind}{{")
+        out.append(f"{ind}    uint32_t y[8];")
+        out.append(f"{ind}    for (int b = 0; b < 8; ++b) y[b] = {src}[b] >> {sh};")
+        mat_apply(out, [f"{dst}[{q}]" for q in range(8)], [f"y[{b}]" for b in range(8)], rows, ind + "    ",
+                  extra=[f"{src}[{q}]" for q in range(8)])
+        out.append(f"{ind}}}")
+
+    out.append(f"template <class F> __device__ __forceinline__ void {st}::epilogue("
+               "const uint32_t (&V)[NL][8], F &&emit) {")
+    # expansion: member (li, k) from V[li] (sq^k) or from the previous member (sq^(k - k')),
+    # computed right before its quad so that few expanded values are live at once
+    prev = {}
+
+    def expand(li, m, k, ind):
+        if k == 0:
+            prev[li] = (f"V[{li}]", 0)
+            return f"V[{li}]"
+        src, kp = prev[li]
+        direct = cost(sqk(k))
+        chained = cost(sqk(k - kp)) if kp else direct
+        out.append(f"{ind}uint32_t W{m}[8];")
+        if kp and chained < direct:
+            mat_apply(out, [f"W{m}[{q}]" for q in range(8)], [f"{src}[{b}]" for b in range(8)], sqk(k - kp), ind)
+        else:
+            mat_apply(out, [f"W{m}[{q}]" for q in range(8)], [f"V[{li}][{b}]" for b in range(8)], sqk(k), ind)
+        prev[li] = (f"W{m}", k)
+        return f"W{m}"
+
+    for qd in range(nq):
+        part = seq[4 * qd:4 * qd + 4]
+        srcs = [expand(li, m, k, I) for li, m, k in part]
+        out.append(f"{I}{{ // quad {qd}: syndromes {[m for _, m, _ in part]}")
+        for j in range(4):
+            out.append(f"{I}    uint32_t F{j}[8];")
+            if j < len(part):
+                fold_level(f"F{j}", srcs[j], a1, 1, I + "    ")
+            else:
+                out.append(f"{I}    for (int b = 0; b < 8; ++b) F{j}[b] = 0u;")
+        for pj in range(2):
+            out.append(f"{I}    uint32_t P{pj}[8], G{pj}[8];")
+            out.append(f"{I}    for (int b = 0; b < 8; ++b) P{pj}[b] = bfi(0x55555555u, "
+                       f"F{2 * pj}[b], F{2 * pj + 1}[b] << 1);")
+            fold_level(f"G{pj}", f"P{pj}", a2, 2, I + "    ")
+        out.append(f"{I}    uint32_t H[8], Q[8];")
+        out.append(f"{I}    for (int b = 0; b < 8; ++b) H[b] = bfi(0x33333333u, G0[b], G1[b] << 2);")
+        fold_level("Q", "H", a4, 4, I + "    ")
+        out.append(f"{I}    emit(std::integral_constant<int, {qd}>{{}}, Q);")
+        out.append(f"{I}}}")
+    out.append("}")
+    return "\n".join(out)
+
+
+def py_split(c: PsCodec):
+    """Split the leaders between the two waves of the pair kernel: each wave owns NL/2 leaders;
+    minimise the larger wave's quad count, then the syndrome imbalance."""
+    from itertools import combinations
+    L = len(c.leaders)
+    sizes = [len(c.members[l]) for l in c.leaders]
+    half = L // 2
+    best = None
+    for comb in combinations(range(L), half):
+        n0 = sum(sizes[i] for i in comb)
+        n1 = sum(sizes) - n0
+        key = (max((n0 + 3) // 4, (n1 + 3) // 4), (n0 + 3) // 4 + (n1 + 3) // 4, abs(n0 - n1))
+        if best is None or key < best[0]:
+            best = (key, comb)
+    own0 = list(best[1])
+    own1 = [i for i in range(L) if i not in own0]
+    return [own0, own1]
+
+
+def gen_py(c: PsCodec):
+    """Pair variant: two waves share 128-position windows of a 256-codeword tile; wave q evaluates
+    ALL leaders over positions [64 q, 64 q + 64) of each window (the PW blocks of those positions:
+    no fixups), then the waves swap the partials of the leaders the other one owns (NL/2 each) and
+    fold their own leaders' syndromes."""
+    gf = c.gf
+    st = f"PY_{c.name}"
+    L = len(c.leaders)
+    assert L % 2 == 0, "pair kernel needs an even leader count"
+    own = py_split(c)
+    NLW = L // 2
+    seqs = []
+    for q in range(2):
+        seq = []
+        for li in sorted(own[q], key=lambda i: -len(c.members[c.leaders[i]])):
+            loc = own[q].index(li)
+            for m, k in sorted(c.members[c.leaders[li]], key=lambda x: x[1]):
+                seq.append((loc, m, k))
+        seqs.append(seq)
+    nq = max((len(s) + 3) // 4 for s in seqs)
+    out = [f"struct {st} : PW_{c.name} {{",
+           f"    static constexpr int NLW = {NLW}, NQW = {nq};",
+           f"    static constexpr int OWN[2][{NLW}] = " + "{" + ", ".join(fmt_list(o) for o in own) + "};",
+           "    // wave Q's syndromes from the totals of its own leaders (T[i] <-> leader OWN[Q][i])",
+           "    template <int Q, class F> static __device__ void epilogue(const uint32_t (&T)[NLW][8], F &&emit);",
+           f"    static constexpr int SYN[2][{nq}][4] = " + "{" + ", ".join(
+               "{" + ", ".join("{" + ", ".join(str(seqs[q][4 * qd + j][1]) if 4 * qd + j < len(seqs[q]) else "-1"
+                                               for j in range(4)) + "}" for qd in range(nq)) + "}"
+               for q in range(2)) + "};",
+           "};"]
+    I = "    "
+    sq_cache = {}
+
+    def sqk(k):
+        if k not in sq_cache:
+            sq_cache[k] = lin_rows(lambda x, k=k: gf.pow(x, 1 << k) if x else 0)
+        return sq_cache[k]
+
+    def cost(rows):
+        return sum(max(0, bin(r).count("1") - 1) for r in rows)
+
+    a1 = lin_rows(lambda x: gf.mul(2, x))
+    a2 = lin_rows(lambda x: gf.mul(4, x))
+    a4 = lin_rows(lambda x: gf.mul(16, x))
+
+    def fold_level(dst, src, rows, sh, ind):
+        out.append(f"{ind}{{")
+        out.append(f"{ind}    uint32_t y[8];")
+        out.append(f"{ind}    for (int b = 0; b < 8; ++b) y[b] = {src}[b] >> {sh};")
+        mat_apply(out, [f"{dst}[{q}]" for q in range(8)], [f"y[{b}]" for b in range(8)], rows, ind + "    ",
+                  extra=[f"{src}[{q}]" for q in range(8)])
+        out.append(f"{ind}}}")
+
+    for q in range(2):
+        seq = seqs[q]
+        out.append(f"template <class F> __device__ __forceinline__ void {st}_epi{q}("
+                   f"const uint32_t (&T)[{st}::NLW][8], F &&emit) {{")
+        prev = {}
+
+        def expand(li, m, k, ind):
+            if k == 0:
+                prev[li] = (f"T[{li}]", 0)
+                return f"T[{li}]"
+            src, kp = prev[li]
+            direct = cost(sqk(k))
+            chained = cost(sqk(k - kp)) if kp else direct
+            out.append(f"{ind}uint32_t W{m}[8];")
+            if kp and chained < direct:
+                mat_apply(out, [f"W{m}[{b}]" for b in range(8)], [f"{src}[{b}]" for b in range(8)], sqk(k - kp), ind)
+            else:
+                mat_apply(out, [f"W{m}[{b}]" for b in range(8)], [f"T[{li}][{b}]" for b in range(8)], sqk(k), ind)
+            prev[li] = (f"W{m}", k)
+            return f"W{m}"
+
+        for qd in range((len(seq) + 3) // 4):
+            part = seq[4 * qd:4 * qd + 4]
+            srcs = [expand(li, m, k, I) for li, m, k in part]
+            out.append(f"{I}{{ // quad {qd}: syndromes {[m for _, m, _ in part]}")
+            for j in range(4):
+                out.append(f"{I}    uint32_t F{j}[8];")
+                if j < len(part):
+                    fold_level(f"F{j}", srcs[j], a1, 1, I + "    ")
+                else:
+                    out.append(f"{I}    for (int b = 0; b < 8; ++b) F{j}[b] = 0u;")
+            for pj in range(2):
+                out.append(f"{I}    uint32_t P{pj}[8], G{pj}[8];")
+                out.append(f"{I}    for (int b = 0; b < 8; ++b) P{pj}[b] = bfi(0x55555555u, "
+                           f"F{2 * pj}[b], F{2 * pj + 1}[b] << 1);")
+                fold_level(f"G{pj}", f"P{pj}", a2, 2, I + "    ")
+            out.append(f"{I}    uint32_t H[8], Q[8];")
+            out.append(f"{I}    for (int b = 0; b < 8; ++b) H[b] = bfi(0x33333333u, G0[b], G1[b] << 2);")
+            fold_level("Q", "H", a4, 4, I + "    ")
+            out.append(f"{I}    emit(std::integral_constant<int, {qd}>{{}}, Q);")
+            out.append(f"{I}}}")
+        out.append("}")
+    out.append(f"template <int Q, class F> __device__ __forceinline__ void {st}::epilogue("
+               "const uint32_t (&T)[NLW][8], F &&emit) {")
+    out.append(f"{I}if constexpr (Q == 0) {st}_epi0(T, emit); else {st}_epi1(T, emit);")
+    out.append("}")
+    return "\n".join(out)
+
+
 def main(dst=None):
     dst = dst or os.path.join(HERE, "..", "csrc", "gen", "ezrs_ps_tables.inc")
     os.makedirs(os.path.dirname(dst), exist_ok=True)
@@ -352,10 +581,12 @@ def main(dst=None):
             "    return (m & a) | (~m & b);", "}"]
     for cd in CODECS:
         body.append(gen_codec(PsCodec(*cd)))
+        body.append(gen_pw(PsCodec(*cd)))
+        body.append(gen_py(PsCodec(*cd)))
     body.append("#define EZRS_PS_CODEC_LIST(X) \\")
     for i, cd in enumerate(CODECS):
         sep = " \\" if i + 1 < len(CODECS) else ""
-        body.append(f"    X(PS_{cd[0]}){sep}")
+        body.append(f"    X({cd[0]}){sep}")
     body.append("} } // namespace ezrs::ps")
     txt = "\n".join(body) + "\n"
     old = open(dst).read() if os.path.exists(dst) else None
