@@ -53,11 +53,15 @@ __device__ unsigned long long g_ps_stamps[8][8][16][8];    // [wg][wave][tile][p
 #define PS_STAMP(ph) do { if (blockIdx.x < 8 && it < 16 && lane == 0) \
     g_ps_stamps[blockIdx.x][wave][it][ph] = __builtin_amdgcn_s_memtime(); } while (0)
 __device__ unsigned long long g_py_stamps[16][2][8][8];  // [wg][wave][tile][phase]
+__device__ unsigned long long g_pg_stamps[16][8][16][8];  // [wg][wave][tile][phase]
+#define PG_STAMP(ph) do { __builtin_amdgcn_sched_barrier(0); if (blockIdx.x < 16 && it < 16 && lane == 0) \
+    g_pg_stamps[blockIdx.x][stamp_wave][it][ph] = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
 #define PY_STAMP(ph) do { __builtin_amdgcn_sched_barrier(0); if (blockIdx.x < 16 && it < 8 && lane == 0) \
     g_py_stamps[blockIdx.x][Q][it][ph] = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
 #else
 #define PS_STAMP(ph) do { } while (0)
 #define PY_STAMP(ph) do { } while (0)
+#define PG_STAMP(ph) do { } while (0)
 #endif
 
 struct PsArgs {
@@ -72,6 +76,9 @@ struct PsArgs {
     int32_t *result;            // decode
     uint8_t *ws;                // decode: [ncw][32] flagged syndromes; encode: [NR][ws_pitch]
     size_t ws_pitch;            // encode: codewords per syndrome row (a multiple of 2048)
+    int ablate;                 // timing experiments only (tools/micro): bit 0 no main loop, 1 no
+                                // exchange, 2 no epilogue, 3 no DMA, 4 no result stores; 0 in the
+                                // library
 };
 
 template <int I, int N, class F> __device__ __forceinline__ void static_for(F &&f) {
@@ -397,18 +404,7 @@ __global__ void __launch_bounds__(kThreads, 4) k_ps_syndromes(PsArgs a) {
     }
 }
 
-// ---- per-wave syndromes ----------------------------------------------------------------------
-// One single-wave workgroup owns a tile of 256 codewords (lane l: rows 4l..4l+3) and every leader:
-// no position slices, so no fixups, no cross-wave reduction and no barriers.  The rows stream
-// through two 8 KiB LDS windows (32 positions x 256 rows); window piece (k, h) -- positions
-// 32W+16h..+15 of row 4l+k -- is DMA'd by lane l to buf + (2k+h) KiB + 16 l, position-aligned
-// (unaligned global addresses are fine for LDS-DMA), and read back by the same lane with one
-// conflict-free ds_read_b128.  Lane l only ever reads what lane l loaded, so a window needs just
-// the wave's own vmcnt.
-constexpr int kPwTile = 256;
-constexpr int kPwWin = 32;                                  // positions per window
-constexpr int kPwWinBytes = kPwTile * kPwWin;               // 8 KiB
-
+// ---- helpers of the gather-layout kernels ------------------------------------------------------
 __device__ __forceinline__ uint32_t lds_addr(const uint8_t *p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t *)p;
 }
@@ -426,240 +422,13 @@ __device__ __forceinline__ pw_rsrc_t pw_rsrc(const uint8_t *base, uint32_t span)
     return r;
 }
 
-// The window's 8 piece loads (LDS-DMA, 16 B per lane).  Inline asm on purpose: the compiler does
-// not see them, so it neither waits for them in front of LDS reads nor counts them -- the kernel's
-// own vm_wait calls do.
-__device__ __forceinline__ void pw_issue(uint8_t *buf, pw_rsrc_t rsrc, uint32_t tile_off,
-                                         const uint32_t (&roff)[4], int pos_rel) {
-    const uint32_t l0 = __builtin_amdgcn_readfirstlane(lds_addr(buf));
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const uint32_t voff = tile_off + roff[k] + (uint32_t)(pos_rel + 16 * h);
-            // (s_nop: an LDS-DMA reading M0 right after an SALU write of M0 is a gfx9 hazard)
-            asm volatile("s_mov_b32 m0, %0\n\t"
-                         "s_nop 0\n\t"
-                         "buffer_load_dwordx4 %1, %2, 0 offen lds"
-                         :: "s"(l0 + (2 * k + h) * 1024), "v"(voff), "s"(rsrc) : "memory", "m0");
-        }
-}
-
-// Fix-ups of a landed window, all rare: pieces that straddle the start or the end of the span
-// come back all-zero (the range check is per piece), so their valid bytes are re-read one by one
-// (first and last rows of a launch); positions before lo (shortened codes) hold the previous
-// row's bytes and are zeroed.  Plain LDS stores: the compiler puts its own vmcnt(0) in front.
-__device__ __forceinline__ void pw_fix(uint8_t *buf, const PsArgs &a, uint32_t tile_off,
-                                       const uint32_t (&roff)[4], int pos_rel, int lane) {
-#pragma unroll 1
-    for (int kh = 0; kh < 8; ++kh) {
-        const int k = kh >> 1, h = kh & 1;
-        const uint32_t rk = k == 0 ? roff[0] : k == 1 ? roff[1] : k == 2 ? roff[2] : roff[3];
-        const int64_t o = (int64_t)tile_off + rk + pos_rel + 16 * h;   // piece start in the span
-        const int64_t r0 = (int64_t)tile_off + rk;                        // row start (position lo)
-        const bool straddle = (o < 0 && o > -16) || (o < (int64_t)a.span && o + 16 > (int64_t)a.span);
-        if (straddle || o < r0) {
-            const uint32_t dst = lds_addr(buf) + kh * 1024 + 16 * lane;
-#pragma unroll 1
-            for (int j = 0; j < 16; ++j) {
-                const int64_t g = o + j;
-                uint32_t v = 0;
-                if (g >= r0 && !straddle) continue;                // the DMA'd byte stands
-                if (g >= r0 && g < (int64_t)a.span) {
-                    // (asm: keep these loads out of the compiler's vmcnt bookkeeping, which
-                    // would otherwise put a vmcnt(0) on the main path where this branch rejoins)
-                    asm volatile("global_load_ubyte %0, %1, off\n\ts_waitcnt vmcnt(0)"
-                                 : "=v"(v) : "v"(a.base + g) : "memory");
-                }
-                asm volatile("ds_write_b8 %0, %1\n\ts_waitcnt lgkmcnt(0)" :: "v"(dst + j), "v"(v) : "memory");
-            }
-        }
-    }
-}
-
-template <int N> __device__ __forceinline__ void vm_wait() {
-    static_assert(N >= 0 && N < 64, "vmcnt field");
-    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
-}
-
-
-// The 4 pieces (rows 4l..4l+3) of one window half: ds_read_b128 at addr + OFF + k * 2 KiB.  Inline
-// asm on purpose: the compiler cannot tell these reads from the LDS-DMA writes in flight to the
-// other window buffer and would otherwise put a vmcnt(0) in front of every LDS read.  The outputs
-// are early-clobber: a destination must not be the address register of a later read.
-template <int OFF>
-__device__ __forceinline__ void lds_read_pieces(uint4 (&R)[4], uint32_t addr) {
-    asm volatile("ds_read_b128 %0, %4 offset:%5\n\t"
-                 "ds_read_b128 %1, %4 offset:%6\n\t"
-                 "ds_read_b128 %2, %4 offset:%7\n\t"
-                 "ds_read_b128 %3, %4 offset:%8\n\t"
-                 "s_waitcnt lgkmcnt(0)"
-                 : "=&v"(R[0]), "=&v"(R[1]), "=&v"(R[2]), "=&v"(R[3])
-                 : "v"(addr), "i"(OFF), "i"(OFF + 2048), "i"(OFF + 4096), "i"(OFF + 6144)
-                 : "memory");
-}
-
-// One window (compile-time W) of the wave's tile: 4 blocks of 8 positions into V; positions
-// >= HI (the next row's bytes; encode: the parity) are masked at compile time.
-template <class C, int W, int HI>
-__device__ __forceinline__ void pw_window(uint32_t (&V)[C::NL][8], const uint8_t *buf, int lane) {
-    static_for<0, 2>([&](auto Hc) {
-        constexpr int h = decltype(Hc)::value;
-        constexpr int p16 = kPwWin * W + 16 * h;
-        if constexpr (p16 < HI) {
-            uint4 R[4];
-            lds_read_pieces<h * 1024>(R, lds_addr(buf) + 16 * lane);
-            uint32_t X[16];
-            {
-                const uint32_t c0[4] = {R[0].x, R[1].x, R[2].x, R[3].x};
-                const uint32_t c1[4] = {R[0].y, R[1].y, R[2].y, R[3].y};
-                const uint32_t c2[4] = {R[0].z, R[1].z, R[2].z, R[3].z};
-                const uint32_t c3[4] = {R[0].w, R[1].w, R[2].w, R[3].w};
-                transpose4x4(c0, X);
-                transpose4x4(c1, X + 4);
-                transpose4x4(c2, X + 8);
-                transpose4x4(c3, X + 12);
-            }
-            static_for<0, 2>([&](auto Bc) {
-                constexpr int p0 = p16 + 8 * decltype(Bc)::value;
-                if constexpr (p0 < HI) {
-                    uint32_t Y[8];
-#pragma unroll
-                    for (int t = 0; t < 8; ++t) Y[t] = p0 + t < HI ? X[p0 - p16 + t] : 0u;
-                    C::template block<p0 / 8>(V, Y);
-                }
-            });
-        }
-    });
-}
-
-// Window pipeline: window j of the wave's sequence sits in buffer j & 1; while window j is
-// computed, window j + 1 (possibly of the next tile) is in flight.
-template <class C, bool ENC>
-__global__ void __attribute__((amdgpu_flat_work_group_size(64, 64), amdgpu_waves_per_eu(2))) k_pw_syndromes(PsArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kPwWinBytes];
-    constexpr int NL = C::NL;
-    const int lane = threadIdx.x;
-    const pw_rsrc_t rsrc = pw_rsrc(a.base, a.span);
-    uint32_t roff[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) roff[k] = (uint32_t)(4 * lane + k) * a.stride;
-    constexpr int HI = ENC ? kN - C::NR : kN;                   // one past the last position
-    constexpr int w_hi = (HI - 1) / kPwWin;
-    const int w_lo = a.lo / kPwWin;                             // windows holding positions lo..HI-1
-    const uint32_t tile_bytes = a.stride * kPwTile;
-    uint32_t tile = blockIdx.x;
-    if (tile >= a.ntiles) return;
-    int j = 0;                                                  // window sequence number
-    pw_issue(lds, rsrc, tile * tile_bytes, roff, kPwWin * w_lo - a.lo);
-    for (; tile < a.ntiles; tile += gridDim.x) {
-        const uint32_t toff = tile * tile_bytes;
-        const bool more = tile + gridDim.x < a.ntiles;
-        uint32_t V[NL][8];
-#pragma unroll
-        for (int s = 0; s < NL; ++s)
-#pragma unroll
-            for (int t = 0; t < 8; ++t) V[s][t] = 0;
-        static_for<0, 8>([&](auto Wc) {
-            constexpr int W = decltype(Wc)::value;
-            if constexpr (W > w_hi) return;
-            else if (W < w_lo) return;                          // wave-uniform
-            uint8_t *cur = lds + (j & 1) * kPwWinBytes;
-            uint8_t *nxt = lds + ((j + 1) & 1) * kPwWinBytes;
-            constexpr bool last = W == w_hi;
-            const bool issue = !last || more;
-            if (issue) {
-                if (!last) pw_issue(nxt, rsrc, toff, roff, kPwWin * (W + 1) - a.lo);
-                else pw_issue(nxt, rsrc, toff + gridDim.x * tile_bytes, roff, kPwWin * w_lo - a.lo);
-                // only the window just issued may stay in flight (LDS-DMA loads complete in order
-                // among themselves; stores in between are not ordered with them, so they are
-                // waited for too)
-                vm_wait<8>();
-            } else {
-                vm_wait<0>();
-            }
-            const int pos_rel = kPwWin * W - a.lo;
-            // wave-uniform test: pieces before a row start (shortened codes) or straddling the
-            // span's end
-            if (__builtin_expect(pos_rel < 0 || (int64_t)toff + tile_bytes + pos_rel + 32 > (int64_t)a.span, 0))
-                pw_fix(cur, a, toff, roff, pos_rel, lane);
-            pw_window<C, W, HI>(V, cur, lane);
-            ++j;
-        });
-        const size_t cw0 = (size_t)tile * kPwTile + 4 * lane;
-        if constexpr (ENC) {
-            // workspace [NR][ws_pitch]: one byte per codeword, 4 codewords per dword store
-            uint8_t *dst = a.ws + cw0;
-            C::epilogue(V, [&](auto Qc, uint32_t (&Q)[8]) {
-                constexpr int qd = decltype(Qc)::value;
-                transpose8(Q);
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) {
-                    constexpr int dummy = 0; (void)dummy;
-                    const int si = C::SYN[qd][jj];
-                    if (si >= 0) *reinterpret_cast<uint32_t *>(dst + (size_t)si * a.ws_pitch) = Q[jj];
-                }
-            });
-        } else {
-            uint32_t D[C::NQ][4];
-            uint32_t nz = 0;
-            C::epilogue(V, [&](auto Qc, uint32_t (&Q)[8]) {
-                constexpr int qd = decltype(Qc)::value;
-                uint32_t vm = 0;
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj)
-                    if (C::SYN[qd][jj] >= 0) vm |= 0x01010101u << jj;
-#pragma unroll
-                for (int t = 0; t < 8; ++t) nz |= Q[t] & vm;
-                transpose8(Q);
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) D[qd][jj] = Q[jj];
-            });
-            uint32_t fl = 0;
-            if (a.neras) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if (cw0 + k < a.ncw && a.neras[cw0 + k]) fl |= 1u << k;
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (nz >> (8 * k) & 0xFF) fl |= 1u << k;
-                if (cw0 + k >= a.ncw) fl &= ~(1u << k);
-            }
-            int32_t res[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) res[k] = (fl >> k & 1) ? kSentinel : 0;
-            if (cw0 + 3 < a.ncw) {
-                *reinterpret_cast<int4 *>(a.result + cw0) = make_int4(res[0], res[1], res[2], res[3]);
-            } else {
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if (cw0 + k < a.ncw) a.result[cw0 + k] = res[k];
-            }
-            if (fl) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    if (!(fl >> k & 1)) continue;
-                    uint8_t *dst = a.ws + (cw0 + k) * 32;
-#pragma unroll
-                    for (int qd = 0; qd < C::NQ; ++qd)
-#pragma unroll
-                        for (int jj = 0; jj < 4; ++jj) {
-                            const int si = C::SYN[qd][jj];
-                            if (si >= 0) dst[si] = (uint8_t)(D[qd][jj] >> (8 * k));
-                        }
-                }
-            }
-        }
-    }
-}
-
 // ---- pair-wave syndromes ---------------------------------------------------------------------
 // Two waves (one workgroup, 4 per CU) own a tile of 256 codewords (lane l: rows l + 64k, byte k
 // of its words) and
 // stream it through ONE 32 KiB LDS window of 128 positions x 256 rows.  Full 128-byte row chunks
 // per DMA instruction (8 lanes per row, 8 rows per instruction) keep the gather at line
-// granularity (narrow per-row pieces measured 1.5-1.8 TB/s: tools/micro/pw_dma.hip).  Wave q
+// granularity (narrow per-row pieces -- a per-wave design with 32-position windows -- measured
+// 1.5-1.8 TB/s for the fetch alone: tools/micro/pw_dma.hip).  Wave q
 // evaluates ALL leaders over the 16-position pieces p = q, q+2, q+4, q+6 of every window (an even
 // split for any codec length) with the blocks of those positions (no fixups), then the waves swap
 // the partials of the leaders the other owns and each folds its own leaders' syndromes (generated
@@ -941,6 +710,292 @@ k_py_syndromes(PsArgs a) {
     else py_body<C, ENC, 1>(a, buf, flags, lane);
 }
 
+// ---- group syndromes (default) -----------------------------------------------------------------
+// NW = 4 waves (one workgroup, 2 per CU) share a whole tile of 256 codewords (lane l: rows
+// l + 64k, byte k of its words) held in LDS in the swizzled gather layout of the pair kernel: two
+// 32 KiB halves (positions 0..127, 128..255), each 128-byte row chunk fetched by 8 lanes of one
+// LDS-DMA instruction.  Fetching both halves of every row together keeps each cache line read
+// once (windows fetched a half at a time re-read the lines the halves share from HBM once the
+// L2 no longer holds them: 3.5-4.4 TB/s vs 6.2-6.7 TB/s, tools/micro/py_dma.hip).  Wave q
+// evaluates ALL leaders over the 16-position pieces g = q, q + 4, q + 8, q + 12 with the PW blocks
+// of those positions (no fixups); two rounds of pairwise exchange through the consumed tile
+// buffer (recursive halving by owner bits: PG4_*::SEND / KEEP) leave each wave the totals of the
+// leaders it owns, whose syndromes it folds.  The next tile is fetched while the epilogues run
+// (and the other workgroup on the CU computes).
+constexpr int kPgTileBytes = 2 * kPyWinBytes;               // 64 KiB
+
+template <class C, bool ENC, int Q>
+__device__ __forceinline__ void pg_body(const PsArgs &a, uint8_t *buf, uint32_t (*flags)[64], int lane) {
+    constexpr int NW = C::NW, NL = C::NL, NLW = C::NLW;
+    constexpr int stamp_wave = Q;
+    (void)stamp_wave;
+    constexpr int NPW = 16 / NW;                                // pieces per wave
+    constexpr int IPW = 32 / NW;                                // DMA instructions per wave per half
+    constexpr int HI = ENC ? kN - C::NR : kN;                   // one past the last position
+    const int w_lo = a.lo / kPyWin;                             // first half holding positions >= lo
+    const pw_rsrc_t rsrc = pw_rsrc(a.base, a.span);
+    const uint32_t lbuf = __builtin_amdgcn_readfirstlane(lds_addr(buf));
+    auto fresh_lane = [&]() { uint32_t l = (uint32_t)lane; asm volatile("" : "+v"(l)); return l; };
+    // DMA: instruction i = 8k + m of a half covers rows 64k + 8m .. +7; lane j -> row 64k + 8m + j/8,
+    // piece (j & 7) ^ f(8m + j/8), f(l) = (l >> 1) & 7 (only depends on m & 1 and j/8)
+    auto doff = [&](uint32_t l, int k, int mp) {
+        const uint32_t dslot = l >> 3;
+        const uint32_t p = (l & 7) ^ ((4 * mp + (dslot >> 1)) & 7);
+        return (64 * k + dslot) * a.stride + 16 * p;
+    };
+    const uint32_t m_step = 8u * a.stride;
+    auto rd = [&](uint32_t l, int p) {                          // piece p of row 64k + l: + 8 KiB k
+        return 1024 * (l >> 3) + 128 * (l & 7) + 16 * (p ^ ((l >> 1) & 7));
+    };
+    const uint32_t tile_bytes = a.stride * kTile;
+
+    auto issue = [&](uint32_t toff) {
+        if (a.ablate & 8) return;
+        const uint32_t l = fresh_lane();
+        for (int w = w_lo; w < 2; ++w) {                        // wave-uniform
+            const uint32_t base = toff + (uint32_t)(kPyWin * w - a.lo);
+#pragma unroll
+            for (int ii = 0; ii < IPW; ii += 2) {
+                const int i = Q * IPW + ii, k = i >> 3, m0 = i & 7;   // m0 even: (m0, m0 + 1)
+                const uint32_t d0 = base + doff(l, k, 0) + m0 * m_step, d1 = base + doff(l, k, 1) + (m0 + 1) * m_step;
+                asm volatile("s_mov_b32 m0, %0\n\t"
+                             "s_nop 0\n\t"
+                             "buffer_load_dwordx4 %1, %2, 0 offen lds"
+                             :: "s"(lbuf + w * kPyWinBytes + i * 1024), "v"(d0), "s"(rsrc) : "memory", "m0");
+                asm volatile("s_mov_b32 m0, %0\n\t"
+                             "s_nop 0\n\t"
+                             "buffer_load_dwordx4 %1, %2, 0 offen lds"
+                             :: "s"(lbuf + w * kPyWinBytes + (i + 1) * 1024), "v"(d1), "s"(rsrc) : "memory", "m0");
+            }
+        }
+    };
+    // fix-ups of this wave's pieces (see pw_fix): straddling the span's ends, or before lo
+    auto fix = [&](uint32_t toff) {
+#pragma unroll 1
+        for (int i = 0; i < 4 * NPW; ++i) {
+            const int k = i & 3, g = Q + NW * (i >> 2), w = g >> 3, p = g & 7;
+            if (w < w_lo) continue;
+            const int64_t r0 = (int64_t)toff + (int64_t)(64 * k + lane) * a.stride;
+            const int64_t o = r0 + kPyWin * w + 16 * p - a.lo;
+            const bool straddle = (o < 0 && o > -16) || (o < (int64_t)a.span && o + 16 > (int64_t)a.span);
+            if (!straddle && o >= r0) continue;
+            const uint32_t dst = lbuf + w * kPyWinBytes + rd(lane, p) + 8192 * k;
+#pragma unroll 1
+            for (int j = 0; j < 16; ++j) {
+                const int64_t gg = o + j;
+                uint32_t v = 0;
+                if (gg >= r0 && !straddle) continue;
+                if (gg >= r0 && gg < (int64_t)a.span)
+                    asm volatile("global_load_ubyte %0, %1, off\n\ts_waitcnt vmcnt(0)"
+                                 : "=&v"(v) : "v"(a.base + gg) : "memory");
+                asm volatile("ds_write_b8 %0, %1\n\ts_waitcnt lgkmcnt(0)" :: "v"(dst + j), "v"(v) : "memory");
+            }
+        }
+    };
+
+    uint32_t pend[ENC ? C::NQW : 1][4];
+    size_t pend_cw0 = 0, pend_col = 0;
+    uint32_t pend_fl = 0;
+    bool pending = false;
+    auto flush = [&]() {
+        if (!pending || (a.ablate & 16)) return;
+        if constexpr (ENC) {
+            uint8_t *dst = a.ws + pend_col;
+#pragma unroll
+            for (int qd = 0; qd < C::NQW; ++qd)
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    const int si = C::SYN[Q][qd][jj];
+                    if (si >= 0) *reinterpret_cast<uint32_t *>(dst + (size_t)si * a.ws_pitch) = pend[qd][jj];
+                }
+        } else if (Q == 0) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (pend_cw0 + 64 * k < a.ncw) a.result[pend_cw0 + 64 * k] = (pend_fl >> k & 1) ? kSentinel : 0;
+        }
+        pending = false;
+    };
+
+    uint32_t tile = blockIdx.x;
+    if (tile < a.ntiles) issue(tile * tile_bytes);
+    for (int it = 0; tile < a.ntiles; tile += gridDim.x, ++it) {
+        (void)it;
+        PG_STAMP(0);
+        const uint32_t toff = tile * tile_bytes;
+        uint32_t V[NL][8];
+#pragma unroll
+        for (int s = 0; s < NL; ++s)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) V[s][t] = 0;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        PG_STAMP(1);
+        __syncthreads();                                         // the tile landed (all waves)
+        PG_STAMP(2);
+        flush();
+        if (__builtin_expect(a.lo > 0 || (int64_t)toff + tile_bytes + kPyWin > (int64_t)a.span, 0)) fix(toff);
+        if (!(a.ablate & 1)) static_for<0, NPW>([&](auto Jc) {
+            constexpr int g = Q + NW * decltype(Jc)::value, w = g >> 3, p = g & 7;
+            constexpr int p16 = kPyWin * w + 16 * p;             // first position of the piece
+            if constexpr (p16 < HI) {
+                if (w < w_lo) return;                            // wave-uniform (shortened codes)
+                uint4 R[4];
+                asm volatile("ds_read_b128 %0, %4\n\t"
+                             "ds_read_b128 %1, %4 offset:8192\n\t"
+                             "ds_read_b128 %2, %4 offset:16384\n\t"
+                             "ds_read_b128 %3, %4 offset:24576\n\t"
+                             "s_waitcnt lgkmcnt(0)"
+                             : "=&v"(R[0]), "=&v"(R[1]), "=&v"(R[2]), "=&v"(R[3])
+                             : "v"(lbuf + w * kPyWinBytes + rd(fresh_lane(), p)) : "memory");
+                uint32_t X[16];
+                {
+                    const uint32_t c0[4] = {R[0].x, R[1].x, R[2].x, R[3].x};
+                    const uint32_t c1[4] = {R[0].y, R[1].y, R[2].y, R[3].y};
+                    const uint32_t c2[4] = {R[0].z, R[1].z, R[2].z, R[3].z};
+                    const uint32_t c3[4] = {R[0].w, R[1].w, R[2].w, R[3].w};
+                    transpose4x4(c0, X);
+                    transpose4x4(c1, X + 4);
+                    transpose4x4(c2, X + 8);
+                    transpose4x4(c3, X + 12);
+                }
+                static_for<0, 2>([&](auto Bc) {
+                    constexpr int p0 = p16 + 8 * decltype(Bc)::value;
+                    if constexpr (p0 < HI) {
+                        uint32_t Y[8];
+#pragma unroll
+                        for (int t = 0; t < 8; ++t) Y[t] = p0 + t < HI ? X[p0 - p16 + t] : 0u;
+                        C::template block<p0 / 8>(V, Y);
+                    }
+                });
+            }
+        });
+        PG_STAMP(3);
+        __syncthreads();                                         // every wave is done with the tile
+        PG_STAMP(4);
+        // recursive-halving exchange through the tile buffer
+        if (!(a.ablate & 2)) static_for<0, C::ROUNDS>([&](auto Rc) {
+            constexpr int r = decltype(Rc)::value, P = Q ^ (1 << r), NS = C::NSEND[r];
+            uint4 *x = reinterpret_cast<uint4 *>(buf);
+#pragma unroll
+            for (int i = 0; i < NS; ++i) {
+                const int s = C::SEND[Q][r][i];
+                if (s < 0) continue;
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    x[((Q * NS + i) * 2 + h) * 64 + lane] =
+                        make_uint4(V[s][4 * h], V[s][4 * h + 1], V[s][4 * h + 2], V[s][4 * h + 3]);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < NS; ++i) {
+                const int s = C::KEEP[Q][r][i];
+                if (s < 0) continue;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const uint4 v = x[((P * NS + i) * 2 + h) * 64 + lane];
+                    V[s][4 * h] ^= v.x;
+                    V[s][4 * h + 1] ^= v.y;
+                    V[s][4 * h + 2] ^= v.z;
+                    V[s][4 * h + 3] ^= v.w;
+                }
+            }
+            __syncthreads();                                     // read before reuse / the next DMA
+        });
+        PG_STAMP(5);
+        if (tile + gridDim.x < a.ntiles) issue(toff + gridDim.x * tile_bytes);
+        uint32_t T[NLW][8];
+#pragma unroll
+        for (int i = 0; i < NLW; ++i)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) T[i][t] = C::OWN[Q][i] >= 0 ? V[C::OWN[Q][i] < 0 ? 0 : C::OWN[Q][i]][t] : 0u;
+        const size_t cw0 = (size_t)tile * kTile + lane;          // byte k <-> codeword cw0 + 64k
+        uint32_t nz = 0;
+        uint32_t D[C::NQW][4];
+#pragma unroll
+        for (int qd = 0; qd < C::NQW; ++qd)
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) D[qd][jj] = T[0][jj + qd];
+        if (!(a.ablate & 4)) C::template epilogue<Q>(T, [&](auto Qc, uint32_t (&Qw)[8]) {
+            constexpr int qd = decltype(Qc)::value;
+            if constexpr (!ENC) {
+                uint32_t vm = 0;
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj)
+                    if (C::SYN[Q][qd][jj] >= 0) vm |= 0x01010101u << jj;
+#pragma unroll
+                for (int t = 0; t < 8; ++t) nz |= Qw[t] & vm;
+            }
+            transpose8(Qw);
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) D[qd][jj] = Qw[jj];
+        });
+        pend_cw0 = cw0;
+        pend_col = (size_t)tile * kTile + 4 * lane;
+        pending = true;
+        PG_STAMP(6);
+        if constexpr (ENC) {
+#pragma unroll
+            for (int qd = 0; qd < C::NQW; ++qd)
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) pend[qd][jj] = D[qd][jj];
+        } else {
+            uint32_t fl = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (nz >> (8 * k) & 0xFF) fl |= 1u << k;
+            // OR over the waves (asm: the compiler would wait for the DMA in flight)
+            const uint32_t fa = lds_addr(reinterpret_cast<uint8_t *>(&flags[Q][lane]));
+            asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" :: "v"(fa), "v"(fl) : "memory");
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < NW; ++q) {
+                if (q == Q) continue;
+                const uint32_t fb = lds_addr(reinterpret_cast<uint8_t *>(&flags[q][lane]));
+                uint32_t fo;
+                asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(fo) : "v"(fb) : "memory");
+                fl |= fo;
+            }
+            if (a.neras) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (cw0 + 64 * k < a.ncw && a.neras[cw0 + 64 * k]) fl |= 1u << k;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (cw0 + 64 * k >= a.ncw) fl &= ~(1u << k);
+            pend_fl = fl;
+            if (fl) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (!(fl >> k & 1)) continue;
+                    uint8_t *dst = a.ws + (cw0 + 64 * k) * 32;
+#pragma unroll
+                    for (int qd = 0; qd < C::NQW; ++qd)
+#pragma unroll
+                        for (int jj = 0; jj < 4; ++jj) {
+                            const int si = C::SYN[Q][qd][jj];
+                            if (si >= 0) dst[si] = (uint8_t)(D[qd][jj] >> (8 * k));
+                        }
+                }
+            }
+        }
+    }
+    flush();
+}
+
+template <class C, bool ENC>
+__global__ void __attribute__((amdgpu_flat_work_group_size(256, 256), amdgpu_waves_per_eu(2)))
+k_pg_syndromes(PsArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t buf[kPgTileBytes];
+    __shared__ uint32_t flags[4][64];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    switch (wave) {
+    case 0: pg_body<C, ENC, 0>(a, buf, flags, lane); break;
+    case 1: pg_body<C, ENC, 1>(a, buf, flags, lane); break;
+    case 2: pg_body<C, ENC, 2>(a, buf, flags, lane); break;
+    default: pg_body<C, ENC, 3>(a, buf, flags, lane); break;
+    }
+}
+
 // ---- encode, stage 2: parity = V^-1 S on 32-codeword bit-sliced registers -------------------
 // Syndromes (encode workspace) -> parity rows.
 // One 256-thread block covers 64 groups of 32 codewords (2048).  Phase 1: wave w transposes
@@ -1039,6 +1094,87 @@ __global__ void __launch_bounds__(256) k_ps_parity(const uint8_t *ws, size_t ws_
     }
 }
 
+
+// 8-wave form of k_ps_parity: wave P computes parity symbols 4P..4P+3 (q_pass4), halving each
+// wave's share of the map and doubling the waves that hide the phases' latencies.
+template <class C, bool PERM>
+__global__ void __launch_bounds__(512) k_ps_parity8(const uint8_t *ws, size_t ws_pitch, uint8_t *parity,
+                                                    size_t pstride, size_t ncw) {
+    constexpr int NR = C::NR;
+    constexpr int kRegion = 32 * NR + 8;                       // bytes per group in the stage
+    constexpr int kPlanes = 8 * NR * kParGroups;               // dwords
+    constexpr int kStage = kParGroups * kRegion / 4;           // dwords
+    constexpr int kLds = kPlanes > kStage ? kPlanes : kStage;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLds];
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const size_t g0 = (size_t)blockIdx.x * kParGroups;
+    const uint8_t *src = ws + (g0 + lane) * 32;                // ws rows are padded to 2048 cw
+    for (int i = wave; i < NR; i += 8) {
+        const uint4 v0 = *reinterpret_cast<const uint4 *>(src + i * ws_pitch);
+        const uint4 v1 = *reinterpret_cast<const uint4 *>(src + i * ws_pitch + 16);
+        uint32_t D[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        transpose8(D);                                         // D[q] bit 8k + m: cw 4m + k
+#pragma unroll
+        for (int qq = 0; qq < 8; ++qq) lds[(8 * i + qq) * 64 + lane] = D[qq];
+    }
+    __syncthreads();
+    uint32_t O[4][8];
+    switch (wave) {
+    case 0: C::template q_pass4<0>(O, lds + lane, 64); break;
+    case 1: if constexpr (C::NPASS4 > 1) C::template q_pass4<1>(O, lds + lane, 64); break;
+    case 2: if constexpr (C::NPASS4 > 2) C::template q_pass4<2>(O, lds + lane, 64); break;
+    case 3: if constexpr (C::NPASS4 > 3) C::template q_pass4<3>(O, lds + lane, 64); break;
+    case 4: if constexpr (C::NPASS4 > 4) C::template q_pass4<4>(O, lds + lane, 64); break;
+    case 5: if constexpr (C::NPASS4 > 5) C::template q_pass4<5>(O, lds + lane, 64); break;
+    case 6: if constexpr (C::NPASS4 > 6) C::template q_pass4<6>(O, lds + lane, 64); break;
+    default: if constexpr (C::NPASS4 > 7) C::template q_pass4<7>(O, lds + lane, 64); break;
+    }
+    __syncthreads();                                           // planes consumed
+    uint8_t *stage = reinterpret_cast<uint8_t *>(lds);
+    if (wave < C::NPASS4) {
+        const int nj = NR - 4 * wave < 4 ? NR - 4 * wave : 4;
+#pragma unroll
+        for (int jl = 0; jl < 4; ++jl)
+            if (jl < nj) transpose8(O[jl]);                    // O[jl][m] byte k: symbol of cw 4m+k
+        uint8_t *reg = stage + lane * kRegion + 4 * wave;
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                uint8_t *row = reg + (4 * m + k) * NR;
+                if (nj == 4) {
+                    *reinterpret_cast<uint32_t *>(row) = gather4(O[0][m], O[1][m], O[2][m], O[3][m], k);
+                } else {
+                    for (int jl = 0; jl < nj; ++jl) row[jl] = (uint8_t)(O[jl][m] >> (8 * k));
+                }
+            }
+    }
+    __syncthreads();
+    const size_t cwb = g0 * 32;
+    for (int r = threadIdx.x; r < kParCw; r += 512) {
+        const size_t x = cwb + r;
+        const size_t k = PERM ? ((x & ~(size_t)255) | ((x & 3) << 6) | ((x >> 2) & 63)) : x;
+        if (k >= ncw) continue;
+        uint8_t *dst = parity + k * pstride;
+        const uint8_t *s8 = stage + (r >> 5) * kRegion + (r & 31) * NR;
+        if constexpr (NR % 8 == 0) {
+#pragma unroll
+            for (int o = 0; o < NR; o += 8) {
+                uint2 v = *reinterpret_cast<const uint2 *>(s8 + o);
+                __builtin_memcpy(dst + o, &v, 8);
+            }
+        } else if constexpr (NR % 4 == 0) {
+#pragma unroll
+            for (int o = 0; o < NR; o += 4) {
+                uint32_t v = *reinterpret_cast<const uint32_t *>(s8 + o);
+                __builtin_memcpy(dst + o, &v, 4);
+            }
+        } else {
+            for (int o = 0; o < NR; ++o) dst[o] = s8[o];
+        }
+    }
+}
+
 } // namespace ps
 
 // ------------------------------------------------------------------------------------------------
@@ -1049,34 +1185,44 @@ template <class C> bool ps_matches(const DevCodec &d) {
            d.poly == C::POLY;
 }
 
-int ps_grid(const DevCodec &d, uint32_t ntiles) {
-    const uint32_t nwg = 2u * (uint32_t)(d.ncu > 0 ? d.ncu : 256);   // 2 workgroups per CU
-    return (int)(ntiles < nwg ? ntiles : nwg);
-}
-
-// Per-wave kernel: 8 single-wave workgroups per CU (16 KiB LDS, <= 256 VGPRs each).
-int pw_grid(const DevCodec &d, uint32_t ntiles) {
-    const uint32_t nwg = 8u * (uint32_t)(d.ncu > 0 ? d.ncu : 256);
-    return (int)(ntiles < nwg ? ntiles : nwg);
-}
-
-// Syndrome kernel variant: 0 = pair (default), 1 = per-wave, 2 = 8-wave slices.  EZRS_PS_VARIANT
-// = pair | wave | slices selects one for comparison runs.
+// Syndrome kernel: 0 = pair (default), 3 = 4-wave group, 2 = 8-wave slices; EZRS_PS_VARIANT =
+// pair | group4 | slices selects one for comparison runs.
 int ps_variant() {
     static const int v = [] {
         const char *e = getenv("EZRS_PS_VARIANT");
-        if (e && std::string(e) == "wave") return 1;
         if (e && std::string(e) == "slices") return 2;
+        if (e && std::string(e) == "group4") return 3;
         return 0;
     }();
     return v;
 }
 
-// Pair kernel: 4 two-wave workgroups per CU (32 KiB LDS, <= 256 VGPRs each).
-int py_grid(const DevCodec &d, uint32_t ntiles) {
-    const uint32_t nwg = 4u * (uint32_t)(d.ncu > 0 ? d.ncu : 256);
-    return (int)(ntiles < nwg ? ntiles : nwg);
+// Workgroups per launch (persistent over tiles): 2 per CU for the 8-wave slices and the 4-wave
+// group kernels (64 KiB LDS each), 4 per CU for the pair kernel (32 KiB each).
+unsigned syn_grid(const DevCodec &d, uint32_t ntiles, int var) {
+    const uint32_t per_cu = var == 0 ? 4u : 2u;
+    const uint32_t nwg = per_cu * (uint32_t)(d.ncu > 0 ? d.ncu : 256);
+    return ntiles < nwg ? ntiles : nwg;
 }
+
+template <class C, bool ENC>
+void launch_syn(int var, unsigned grid, const ps::PsArgs &p, hipStream_t s) {
+    if (var == 0)
+        hipLaunchKernelGGL((ps::k_py_syndromes<typename C::PY, ENC>), dim3(grid), dim3(128), 0, s, p);
+    else if (var == 3)
+        hipLaunchKernelGGL((ps::k_pg_syndromes<typename C::PG4, ENC>), dim3(grid), dim3(256), 0, s, p);
+    else
+        hipLaunchKernelGGL((ps::k_ps_syndromes<typename C::PS, ENC>), dim3(grid), dim3(ps::kThreads), 0, s, p);
+}
+
+#define EZRS_PS_TRIPLE(C)                                                                         \
+    struct T_##C {                                                                                \
+        using PS = ps::PS_##C;                                                                    \
+        using PY = ps::PY_##C;                                                                    \
+        using PG4 = ps::PG4_##C;                                                                  \
+    };
+EZRS_PS_CODEC_LIST(EZRS_PS_TRIPLE)
+#undef EZRS_PS_TRIPLE
 
 } // namespace
 
@@ -1109,6 +1255,7 @@ bool ps_can_decode(const DevCodec &d, const DecodeArgs &a) {
 
 hipError_t launch_ps_encode(int id, const DevCodec &d, const EncodeArgs &a, void *ws, hipStream_t s) {
     const size_t maxr = ps_max_rows(a.data_stride);
+    const int var = ps_variant();
     for (size_t k0 = 0; k0 < a.ncw; k0 += maxr) {
         const size_t n = a.ncw - k0 < maxr ? a.ncw - k0 : maxr;
         ps::PsArgs p{};
@@ -1122,29 +1269,20 @@ hipError_t launch_ps_encode(int id, const DevCodec &d, const EncodeArgs &a, void
         p.ws = static_cast<uint8_t *>(ws);
         p.ws_pitch = ps_pitch(n);
         uint8_t *par = static_cast<uint8_t *>(a.parity) + k0 * a.parity_stride;
-        const unsigned grid = (unsigned)ps_grid(d, p.ntiles);
-        const unsigned wgrid = (unsigned)pw_grid(d, p.ntiles);
-        const unsigned ygrid = (unsigned)py_grid(d, p.ntiles);
+        const unsigned grid = syn_grid(d, p.ntiles, var);
         const unsigned pgrid = (unsigned)((n + ps::kParCw - 1) / ps::kParCw);
-        const int var = ps_variant();
         int k = 0;
+        // syndromes of the data positions, then parity = V^-1 S (the pair and group kernels leave
+        // the workspace in tile-lane column order: PERM)
 #define EZRS_PS_ENC(C)                                                                            \
         if (k++ == id) {                                                                          \
-            if (var == 0)                                                                         \
-                hipLaunchKernelGGL((ps::k_py_syndromes<ps::PY_##C, true>), dim3(ygrid), dim3(128),\
-                                   0, s, p);                                                     \
-            else if (var == 1)                                                                    \
-                hipLaunchKernelGGL((ps::k_pw_syndromes<ps::PW_##C, true>), dim3(wgrid), dim3(64), \
-                                   0, s, p);                                                     \
-            else                                                                                  \
-                hipLaunchKernelGGL((ps::k_ps_syndromes<ps::PS_##C, true>), dim3(grid), dim3(ps::kThreads), \
-                                   0, s, p);                                                     \
-            if (var == 0)                                                                         \
-                hipLaunchKernelGGL((ps::k_ps_parity<ps::PS_##C, true>), dim3(pgrid), dim3(256), 0, s,\
+            launch_syn<T_##C, true>(var, grid, p, s);                                             \
+            if (var == 2)                                                                         \
+                hipLaunchKernelGGL((ps::k_ps_parity8<ps::PS_##C, false>), dim3(pgrid), dim3(512), 0, s, \
                                    static_cast<const uint8_t *>(ws), p.ws_pitch, par, a.parity_stride, n); \
             else                                                                                  \
-            hipLaunchKernelGGL((ps::k_ps_parity<ps::PS_##C, false>), dim3(pgrid), dim3(256), 0, s,   \
-                               static_cast<const uint8_t *>(ws), p.ws_pitch, par, a.parity_stride, n); \
+                hipLaunchKernelGGL((ps::k_ps_parity8<ps::PS_##C, true>), dim3(pgrid), dim3(512), 0, s, \
+                                   static_cast<const uint8_t *>(ws), p.ws_pitch, par, a.parity_stride, n); \
         }
         EZRS_PS_CODEC_LIST(EZRS_PS_ENC)
 #undef EZRS_PS_ENC
@@ -1157,6 +1295,7 @@ hipError_t launch_ps_encode(int id, const DevCodec &d, const EncodeArgs &a, void
 hipError_t launch_ps_syndromes(int id, const DevCodec &d, const DecodeArgs &a, uint8_t *syn_ws,
                                hipStream_t s) {
     const size_t maxr = ps_max_rows(a.data_stride);
+    const int var = ps_variant();
     for (size_t k0 = 0; k0 < a.ncw; k0 += maxr) {
         const size_t n = a.ncw - k0 < maxr ? a.ncw - k0 : maxr;
         ps::PsArgs p{};
@@ -1170,23 +1309,10 @@ hipError_t launch_ps_syndromes(int id, const DevCodec &d, const DecodeArgs &a, u
         p.neras = a.neras ? a.neras + k0 : nullptr;
         p.result = a.result + k0;
         p.ws = syn_ws + k0 * 32;
-        const unsigned grid = (unsigned)ps_grid(d, p.ntiles);
-        const unsigned wgrid = (unsigned)pw_grid(d, p.ntiles);
-        const unsigned ygrid = (unsigned)py_grid(d, p.ntiles);
-        const int var = ps_variant();
+        const unsigned grid = syn_grid(d, p.ntiles, var);
         int k = 0;
 #define EZRS_PS_SYN(C)                                                                            \
-        if (k++ == id) {                                                                          \
-            if (var == 0)                                                                         \
-                hipLaunchKernelGGL((ps::k_py_syndromes<ps::PY_##C, false>), dim3(ygrid), dim3(128),\
-                                   0, s, p);                                                     \
-            else if (var == 1)                                                                    \
-                hipLaunchKernelGGL((ps::k_pw_syndromes<ps::PW_##C, false>), dim3(wgrid), dim3(64),\
-                                   0, s, p);                                                     \
-            else                                                                                  \
-                hipLaunchKernelGGL((ps::k_ps_syndromes<ps::PS_##C, false>), dim3(grid), dim3(ps::kThreads),\
-                                   0, s, p);                                                     \
-        }
+        if (k++ == id) launch_syn<T_##C, false>(var, grid, p, s);
         EZRS_PS_CODEC_LIST(EZRS_PS_SYN)
 #undef EZRS_PS_SYN
         hipError_t e = hipGetLastError();

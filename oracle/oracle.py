@@ -20,6 +20,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 ORACLE_SO = os.path.join(HERE, "_build", "libezrs_oracle.so")
 REF_SO = os.path.join(HERE, "_ref", "libezrs_ref.so")
+KARN_SO = os.path.join(HERE, "_ref", "libkarn.so")
 
 _vp, _sz, _u, _i = C.c_void_p, C.c_size_t, C.c_uint, C.c_int
 
@@ -235,6 +236,75 @@ class Ref:
         b = np.zeros(256, np.uint8)
         cls.lib().ezref_dual_tables(_ptr(a), _ptr(b))
         return a, b
+
+
+# ---------------------------------------------------------------------------------------------
+class Karn:
+    """Phil Karn's libfec RS codecs (fec-3.0.1: init/encode/decode_rs_char, encode/decode_rs_8,
+    encode/decode_rs_ccsds) compiled from the reference's tarball by oracle/Makefile (karn); only
+    tests/golden/make_karn_fixtures.py calls it -- the committed fixtures carry its outputs."""
+
+    _L = None
+
+    @classmethod
+    def available(cls):
+        return os.path.exists(KARN_SO)
+
+    @classmethod
+    def lib(cls):
+        if cls._L is None:
+            L = C.CDLL(KARN_SO)
+            L.karn_init_char.restype = _vp
+            L.karn_init_char.argtypes = [_i, _i, _i, _i, _i, _i]
+            L.karn_free_char.argtypes = [_vp]
+            L.karn_encode_char_batch.argtypes = [_vp, _vp, C.c_long, _vp, C.c_long, C.c_long, _i]
+            L.karn_decode_char_batch.argtypes = [_vp, _vp, C.c_long, C.c_long, _i, _vp, _vp, _vp]
+            for f in ("karn_encode_8_batch", "karn_encode_ccsds_batch"):
+                getattr(L, f).argtypes = [_vp, C.c_long, _vp, C.c_long, C.c_long, _i]
+            for f in ("karn_decode_8_batch", "karn_decode_ccsds_batch"):
+                getattr(L, f).argtypes = [_vp, C.c_long, C.c_long, _vp, _vp, _vp, _i]
+            cls._L = L
+        return cls._L
+
+    @classmethod
+    def encode_char(cls, params, data, length):
+        """params = (symsize, gfpoly, fcr, prim, nroots, pad); data uint8 [ncw, >= length]."""
+        L = cls.lib()
+        rs = L.karn_init_char(*params)
+        assert rs, "init_rs_char rejected the parameters"
+        ncw = data.shape[0]
+        par = np.zeros((ncw, params[4]), np.uint8)
+        L.karn_encode_char_batch(rs, _ptr(data), data.shape[1], _ptr(par), par.shape[1], ncw, length)
+        L.karn_free_char(rs)
+        return par
+
+    @classmethod
+    def decode_char(cls, params, rows, eras, neras):
+        """rows uint8 [ncw, len + nroots] corrected in place; eras int32 [ncw, nroots] in/out."""
+        L = cls.lib()
+        rs = L.karn_init_char(*params)
+        ncw = rows.shape[0]
+        result = np.zeros(ncw, np.int32)
+        L.karn_decode_char_batch(rs, _ptr(rows), rows.shape[1], ncw, params[4], _ptr(eras), _ptr(neras),
+                                 _ptr(result))
+        L.karn_free_char(rs)
+        return result
+
+    @classmethod
+    def encode_fixed(cls, kind, data, pad=0):
+        """kind "8" (conventional basis, 0x187 / fcr 112 / prim 11) or "ccsds" (dual basis)."""
+        ncw = data.shape[0]
+        par = np.zeros((ncw, 32), np.uint8)
+        getattr(cls.lib(), f"karn_encode_{kind}_batch")(_ptr(data), data.shape[1], _ptr(par), 32, ncw, pad)
+        return par
+
+    @classmethod
+    def decode_fixed(cls, kind, rows, eras, neras, pad=0):
+        ncw = rows.shape[0]
+        result = np.zeros(ncw, np.int32)
+        getattr(cls.lib(), f"karn_decode_{kind}_batch")(_ptr(rows), rows.shape[1], ncw, _ptr(eras), _ptr(neras),
+                                                        _ptr(result), pad)
+        return result
 
 
 # ---------------------------------------------------------------------------------------------

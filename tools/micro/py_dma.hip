@@ -85,7 +85,6 @@ int main() {
         unsigned grid = ncu * PC < ntiles ? ncu * PC : ntiles;                                         \
         float ms = timeit([&] { hipLaunchKernelGGL((k_py_dma<WV, D, WIN>), dim3(grid), dim3(64 * WV), 0, 0, d, span, ncw, out, spin); }); \
         printf("W=%3d waves/WG %d D=%d WG/CU %d spin %4d: %7.1f us %5.2f TB/s\n", WIN, WV, D, PC, spin, ms * 1e3, gb / ms); }
-    RUN(2, 1, 4, 128) RUN(2, 2, 4, 64) RUN(2, 3, 3, 64) RUN(2, 2, 2, 128) RUN(4, 2, 2, 64) RUN(4, 3, 1, 128) RUN(8, 2, 1, 128)
-    RUN(8, 4, 1, 64) RUN(4, 4, 2, 64) RUN(2, 4, 2, 64) RUN(8, 3, 1, 128) RUN(4, 2, 1, 128)
+    RUN(4, 1, 2, 256) RUN(8, 1, 1, 256) RUN(8, 2, 1, 256) RUN(2, 1, 2, 256) RUN(4, 2, 1, 256) RUN(4, 1, 2, 128) RUN(2, 1, 4, 128)
     return 0;
 }
