@@ -467,6 +467,79 @@ def harness_check(args):
         dist.destroy_process_group()
 
 
+def bench_shards(args):
+    """SURVEY.md 8d C2 shard batches: S-byte shards (S = 1 KiB .. 1 MiB) split into 223-byte data
+    chunks, each chunk + 32 parity bytes one RS(255,223) row, the last chunk of a shard shortened.
+    The full rows of every shard in the batch go in one call, the shortened tails in a second one
+    (the documented tail call; a shortened RS(255,223) row is a valid codeword of the same codec,
+    rs_base:1170-1242).  Batches are sized to ~256 MB of shard data per GPU (device-resident);
+    per S the line reports the encode+decode rate of shard bytes and each call's HBM fraction."""
+    import torch
+    import ezrs
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    codec = ezrs.Codec.rs(N, K, device=local)
+    gen = torch.Generator(device="cuda").manual_seed(0x5EED0003)
+    sweep = []
+    for S in (1 << 10, 1 << 14, 1 << 18, 1 << 20):
+        shards = max(1, (256 << 20) // S)
+        full, tail = S // K, S % K
+        rows = torch.randint(0, 256, (shards * full, N), generator=gen, device="cuda",
+                             dtype=torch.int32).to(torch.uint8)
+        trows = (torch.randint(0, 256, (shards, tail + NR), generator=gen, device="cuda",
+                               dtype=torch.int32).to(torch.uint8) if tail else None)
+        codec.reserve(max(rows.shape[0], shards))
+        r1 = torch.empty(rows.shape[0], dtype=torch.int32, device="cuda")
+        r2 = torch.empty(shards, dtype=torch.int32, device="cuda")
+        stream = torch.cuda.current_stream()
+
+        def step(ev=None):
+            if ev:
+                ev[0].record(stream)
+            codec.encode(rows, K, stream=stream)
+            if trows is not None:
+                codec.encode(trows, tail, stream=stream)
+            if ev:
+                ev[1].record(stream)
+            codec.decode(rows, K, result=r1, stream=stream)
+            if trows is not None:
+                codec.decode(trows, tail, result=r2, stream=stream)
+            if ev:
+                ev[2].record(stream)
+        for _ in range(max(1, args.warmup)):
+            step()
+        torch.cuda.synchronize()
+        if int((r1 != 0).sum()) or (trows is not None and int((r2 != 0).sum())):
+            raise SystemExit(f"shards S={S}: encoded rows did not decode clean")
+        steps = max(1, args.steps)
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+        t0 = time.perf_counter()
+        for i in range(steps):
+            step(evs[i])
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+        enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / steps
+        dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / steps
+        ncw_total = rows.shape[0] + (shards if tail else 0)
+        enc_alg = shards * (S + NR * (full + (1 if tail else 0)))    # data read + parity written
+        dec_alg = enc_alg + 4 * ncw_total                              # all read + result written
+        sweep.append({"shard_bytes": S, "shards": shards, "codewords": ncw_total,
+                      "tail_len": tail, "gbs_shard_data": round(shards * S / dt / 1e9, 3),
+                      "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4),
+                      "frac_encode": round(enc_alg / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                      "frac_decode": round(dec_alg / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
+        log(f"shards S={S}: {sweep[-1]}")
+        del rows, trows
+    best = max(sweep, key=lambda r: r["gbs_shard_data"])
+    print(json.dumps({"metric": "RS(255,223) shard-batch encode+decode GB/s device-resident (sweep)",
+                      "value": best["gbs_shard_data"], "unit": "GB/s", "n_gpus": 1,
+                      "steps": args.steps, "warmup": args.warmup, "higher_is_better": True,
+                      "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+                      "config": {"workload": "C2 shard batches: S-byte shards, ~256 MB per step",
+                                 "codec": "RS(255,223) poly 0x11d fcr 1 prim 1"},
+                      "sweep": sweep}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -477,9 +550,11 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=3.0,
                     help="seconds per CPU-baseline measurement (5 configs x 1/all threads)")
     ap.add_argument("--e2e", action="store_true", help="also time the host-memory pipeline")
-    ap.add_argument("--workload", choices=("c2", "c3", "c4", "c5"), default="c2",
-                    help="c2: the headline RS(255,223) line; c3: RS(255,223) 8 errors + 4 erasures "
-                         "decode; c4: RS(65535,65503); c5: BCH(1023,983,4) (SURVEY.md 8d)")
+    ap.add_argument("--workload", choices=("c2", "c1", "c3", "c4", "c5", "shards"), default="c2",
+                    help="c2: the headline RS(255,223) line; c1: the same for RS(255,251); c3: "
+                         "RS(255,223) 8 errors + 4 erasures decode; c4: RS(65535,65503); c5: "
+                         "BCH(1023,983,4) (SURVEY.md 8d); shards: RS(255,223) over S-byte shards, "
+                         "S = 1 KiB .. 1 MiB (full codewords + one shortened tail call per shard)")
     ap.add_argument("--harness-check", action="store_true",
                     help="CPU/gloo check of the multi-rank harness (placeholder step, no GPU)")
     args = ap.parse_args()
@@ -493,6 +568,8 @@ def main():
         return bench_c5(args)
     if args.workload in ("c3", "c4"):
         return bench_rs_errors(args)
+    if args.workload == "shards":
+        return bench_shards(args)
 
     import torch
     import torch.distributed as dist
@@ -506,11 +583,13 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    codec = ezrs.Codec.rs(N, K, device=local)
+    n, k = (255, 251) if args.workload == "c1" else (N, K)
+    enc_bytes, dec_bytes = n, n + 4               # encode: k read + n-k written; decode: n read + result
+    codec = ezrs.Codec.rs(n, k, device=local)
     ncw = args.ncw
     codec.reserve(ncw)
     gen = torch.Generator(device="cuda").manual_seed(0x5EED0002 + rank)
-    cw = torch.randint(0, 256, (ncw, N), generator=gen, device="cuda", dtype=torch.int32)
+    cw = torch.randint(0, 256, (ncw, n), generator=gen, device="cuda", dtype=torch.int32)
     cw = cw.to(torch.uint8)
     result = torch.empty(ncw, dtype=torch.int32, device="cuda")
     stream = torch.cuda.current_stream()
@@ -518,10 +597,10 @@ def main():
     def step(ev=None):
         if ev:
             ev[0].record(stream)
-        codec.encode(cw, K, stream=stream)
+        codec.encode(cw, k, stream=stream)
         if ev:
             ev[1].record(stream)
-        codec.decode(cw, K, result=result, stream=stream)
+        codec.decode(cw, k, result=result, stream=stream)
         if ev:
             ev[2].record(stream)
 
@@ -548,11 +627,11 @@ def main():
     elapsed = shard.max_over_ranks(elapsed, device="cuda")
 
     total_cw = ncw * world * args.steps
-    value = total_cw * N / elapsed / 1e9
+    value = total_cw * n / elapsed / 1e9
     if enc_ms >= dec_ms:
-        dom, ms, per_cw = "ezrs_encode", enc_ms, ENC_BYTES
+        dom, ms, per_cw = "ezrs_encode", enc_ms, enc_bytes
     else:
-        dom, ms, per_cw = "ezrs_decode", dec_ms, DEC_BYTES
+        dom, ms, per_cw = "ezrs_decode", dec_ms, dec_bytes
     achieved = ncw * per_cw / (ms * 1e-3) / 1e9
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -563,20 +642,20 @@ def main():
     e2e = None
     if args.e2e and rank == 0:
         import numpy as np
-        h = np.random.default_rng(3).integers(0, 256, (ncw, N)).astype(np.uint8)
+        h = np.random.default_rng(3).integers(0, 256, (ncw, n)).astype(np.uint8)
         # pinned (page-locked, hipHostMalloc via torch) copy of the same batch: the north_star's
         # "pinned hipMemcpyAsync" end-to-end rate; the pageable numpy rate is reported beside it
         hp = torch.from_numpy(h.copy()).pin_memory().numpy()
         e2e = {}
         for name, buf in (("pageable", h), ("pinned", hp)):
-            codec.encode_host(buf, K)
+            codec.encode_host(buf, k)
             t1 = time.perf_counter()
             for _ in range(3):
-                codec.encode_host(buf, K)
-                r = codec.decode_host(buf, K)
+                codec.encode_host(buf, k)
+                r = codec.decode_host(buf, k)
             dt = (time.perf_counter() - t1) / 3
             assert (r == 0).all()
-            e2e[name] = round(ncw * N / dt / 1e9, 3)
+            e2e[name] = round(ncw * n / dt / 1e9, 3)
             log(f"host-memory ({name}) encode+decode: {e2e[name]} GB/s")
 
     cpu = None
@@ -584,15 +663,16 @@ def main():
         cpu = cpu_baselines(args.cpu_seconds)
 
     if rank == 0:
-        line = {"metric": "RS(255,223) encode+decode GB/s device-resident",
+        line = {"metric": f"RS({n},{k}) encode+decode GB/s device-resident",
                 "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
                 "dtype": "u8", "data": "synthetic",
-                "config": {"workload": "C2: RS(255,223) encode + clean decode, 1M codewords/GPU",
-                           "codec": "RS(255,223) poly 0x11d fcr 1 prim 1",
+                "config": {"workload": f"{args.workload.upper()}: RS({n},{k}) encode + clean decode, "
+                                       f"{ncw} codewords/GPU",
+                           "codec": f"RS({n},{k}) poly 0x11d fcr 1 prim 1",
                            "codewords_per_gpu": ncw, "global_codewords": ncw * world,
-                           "bytes_per_codeword": N, "parallelism": f"shard{world}"},
+                           "bytes_per_codeword": n, "parallelism": f"shard{world}"},
                 "roofline": roofline, "cpu_baseline": cpu}
         if e2e is not None:
             line["e2e_host_gbs"] = e2e

@@ -1,0 +1,296 @@
+// ezrs_errors.hip -- the error path behind the sliced GF(2^8) syndrome kernels: decodes the
+// codewords whose syndromes are not all zero (or that carry erasures), starting from the syndromes
+// those kernels left in the workspace.
+//
+// Same algorithm, same branch structure and same outputs as decode_symbols (c++/ezpwd/rs_base:
+// 1335-1718): erasure locator (1436-1450), Berlekamp-Massey with the reference's length rule
+// (1507-1546), Chien in the reference's root order (1555-1584), Omega (1596-1604), Forney with
+// in-place correction and partial fixes kept on failure (1610-1690), positions (1700-1716).
+//
+// Organisation for CDNA4 (m = 8, NR <= 32):
+//  * One wavefront screens 256 result slots (a 16-byte load per lane), compacts the flagged ones into
+//    an LDS list with ballots, and decodes them 64 at a time, one codeword per lane: a sparse batch
+//    keeps every lane busy, a dense one (C3: every codeword flagged) runs at full width.
+//  * All working polynomials (lambda, B, log lambda, Chien registers, Omega) live in VGPRs: every
+//    loop over coefficients is unrolled, so every index is a constant; coefficient blocks of 8 above
+//    the current degree bound are skipped (deg lambda, deg B <= r - 1 at BM step r).  Only the
+//    syndromes (read at the run-time offset r - 1 - i) and the Chien roots are per-lane LDS arrays.
+//  * GF products through a 256-byte antilog table in LDS (one dword per bank: conflict-free for any
+//    64 indices) with a zero class for log(0): any log >= 510 marks zero, and a product's index is
+//    min(x, x - 255, 255) with alpha_to[255] = 0, so no compare/select per product.
+#include "ezrs_internal.hpp"
+
+namespace ezrs {
+namespace {
+
+constexpr int32_t kSentinel = INT32_MIN;
+constexpr int kSpan = 256;              // result slots screened per wavefront
+constexpr unsigned kZ = 1024;           // log(0); every value >= 510 is in the zero class
+constexpr int kSrows = 40;              // reversed syndromes: rows 0..31, zero-class padding 32..39
+
+// antilog index of the product of two logs (either may be in the zero class)
+__device__ __forceinline__ unsigned pidx(unsigned x) {
+    const unsigned y = x - 255u;
+    return min(min(x, y), 255u);
+}
+// (x + y) mod 255 for x, y in [0, 254]
+__device__ __forceinline__ unsigned addmod(unsigned x, unsigned y) {
+    const unsigned s = x + y;
+    return min(s, s - 255u);
+}
+
+struct Lds {
+    uint8_t A[256];                      // alpha_to, A[255] = 0
+    uint16_t I[256];                     // index_of, I[0] = kZ
+    uint32_t list[kSpan];                // flagged codewords of this wave's span
+    uint16_t srev[kSrows * 64];          // [row][lane]: row k holds S_{31-k} (log), rows >= 32 kZ
+    uint8_t root[32 * 64];               // [j][lane]: Chien roots in order
+};
+
+__device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, Lds &L, const unsigned lane, uint8_t *data, unsigned len,
+                           uint8_t *parity, const uint32_t *eras, unsigned no_eras, uint32_t *pos_out,
+                           uint8_t *corr_out, const uint8_t *syn_in) {
+    const unsigned NR = c.nroots, LOAD = c.load, FCR = c.fcr, PRM = c.prim;
+    if (len == 0 || len > LOAD) return -1;                                    // 1375-1377
+    if (no_eras > NR) return -1;                                              // 1380-1382
+    for (unsigned i = 0; i < no_eras; ++i)
+        if (eras[i] >= len + NR) return -1;                                   // 1383-1387
+    const unsigned pad = LOAD - len;
+    auto S = [&](int k) -> uint16_t & { return L.srev[k * 64 + lane]; };
+
+    // syndromes (polynomial form from the syndrome kernel) -> logs, stored reversed (1416-1434)
+    unsigned syn_error = 0;
+    {
+        uint4 w0, w1;
+        __builtin_memcpy(&w0, syn_in, 16);
+        __builtin_memcpy(&w1, syn_in + 16, 16);
+        const unsigned w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+            const unsigned v = i < (int)NR ? (w[i >> 2] >> (8 * (i & 3))) & 255u : 0u;
+            syn_error |= v;
+            S(31 - i) = L.I[v];
+        }
+#pragma unroll
+        for (int k = 32; k < kSrows; ++k) S(k) = kZ;
+    }
+    if (!syn_error) return 0;
+
+    // erasure locator (1436-1450): lambda in polynomial form, lam[0] == 1
+    unsigned lam[33];
+#pragma unroll
+    for (int i = 0; i <= 32; ++i) lam[i] = i == 0;
+    if (no_eras > 0) {
+        lam[1] = L.A[(PRM * (c.nn - 1 - (eras[0] + pad))) % 255u];
+        for (unsigned e = 1; e < no_eras; ++e) {
+            const unsigned u = (PRM * (c.nn - 1 - (eras[e] + pad))) % 255u;
+            // lam[j] ^= lam[j-1] * alpha^u for j = e+1 .. 1 (lam[j-1] == 0 above j - 1 > e)
+#pragma unroll
+            for (int j0 = 32; j0 >= 0; j0 -= 8) {
+                if ((unsigned)(j0 > 0 ? j0 - 1 : 0) <= e) {
+#pragma unroll
+                    for (int j = j0 + 7; j >= j0; --j) {
+                        if (j < 1 || j > 32) continue;
+                        lam[j] ^= L.A[pidx(u + L.I[lam[j - 1]])];
+                    }
+                }
+            }
+        }
+    }
+    unsigned b[33], l[33];
+#pragma unroll
+    for (int i = 0; i <= 32; ++i) b[i] = i == 0 ? 0u : L.I[lam[i]];
+
+    // Berlekamp-Massey (1507-1546).  At step r, lambda and B have degree <= r - 1.
+    unsigned el = no_eras;
+    for (unsigned r = no_eras + 1; r <= NR; ++r) {
+        const int sb = 32 - (int)r;           // row of S_{r-1}; S_{r-1-i} at row sb + i
+        unsigned discr = 0;
+#pragma unroll
+        for (int i0 = 0; i0 <= 32; i0 += 8) {
+            if ((unsigned)i0 <= r) {
+#pragma unroll
+                for (int i = i0; i < i0 + 8 && i <= 32; ++i) {
+                    l[i] = i == 0 ? 0u : L.I[lam[i]];
+                    if (i < 32) discr ^= L.A[pidx(l[i] + S(sb + i))];
+                }
+            }
+        }
+        const unsigned dl = L.I[discr];
+        const bool upd = dl < 510u && 2 * el <= r + no_eras - 1;
+        const unsigned ndl = 255u - dl;
+#pragma unroll
+        for (int i0 = 32; i0 >= 0; i0 -= 8) {
+            if ((unsigned)i0 <= r) {
+#pragma unroll
+                for (int i = i0 + 7; i >= i0; --i) {
+                    if (i > 32) continue;
+                    const unsigned bp = i > 0 ? b[i - 1] : kZ;
+                    if (i > 0) lam[i] ^= L.A[pidx(dl + bp)];
+                    const unsigned d = l[i] + ndl;
+                    const unsigned nb = min(min(d, d - 255u), kZ);
+                    b[i] = upd ? nb : bp;
+                }
+            }
+        }
+        el = upd ? r + no_eras - el : el;
+    }
+
+    // lambda to index form, its degree (1549-1553)
+    unsigned deg = 0;
+#pragma unroll
+    for (int i = 0; i <= 32; ++i) {
+        l[i] = i == 0 ? 0u : L.I[lam[i]];
+        if (i > 0 && lam[i] != 0) deg = i;
+    }
+
+    // Chien search (1555-1584): registers reg_j = log lambda_j + j*i (mod 255), roots in order
+    int count = 0;
+    if (deg > 0) {
+        unsigned rg[33];
+#pragma unroll
+        for (int j = 1; j <= 32; ++j) rg[j] = l[j] < 255u ? l[j] : 0x80000000u;
+        for (unsigned i = 1; i <= 255; ++i) {
+            unsigned q = 1;
+#pragma unroll
+            for (int j0 = 1; j0 <= 32; j0 += 8) {
+                if ((unsigned)j0 <= deg) {
+#pragma unroll
+                    for (int j = j0; j < j0 + 8; ++j) {
+                        const unsigned a = rg[j] + j, z = rg[j] + (j - 255u);
+                        rg[j] = min(a, z);
+                        q ^= L.A[min(rg[j], 255u)];
+                    }
+                }
+            }
+            if (q != 0) continue;
+            L.root[count * 64 + lane] = (uint8_t)i;
+            if (++count == (int)deg) break;
+        }
+    }
+    const int nroot = count;
+    if ((int)deg != count || deg == 0) count = -1;                           // 1577-1595
+
+    if (count > 0) {
+        // Omega = S * lambda mod x^(deg lambda), index form (1596-1604)
+        const unsigned deg_omega = deg - 1;
+        unsigned om[32];
+#pragma unroll
+        for (int i0 = 0; i0 < 32; i0 += 8) {
+            if ((unsigned)i0 <= deg_omega) {
+#pragma unroll
+                for (int i = i0; i < i0 + 8; ++i) {
+                    unsigned t = 0;
+#pragma unroll
+                    for (int j = 0; j <= i; ++j) t ^= L.A[pidx(S(31 - (i - j)) + l[j])];
+                    om[i] = L.I[t];
+                }
+            }
+        }
+        const unsigned top = (deg < NR - 1 ? deg : NR - 1) & ~1u;
+        // Forney, roots in reverse order, corrections applied as found (1610-1690)
+        for (int j = count - 1; j >= 0; --j) {
+            const unsigned rj = L.root[j * 64 + lane];
+            unsigned num1 = 0, den = 0, e = 0;     // e = i * rj (mod 255)
+#pragma unroll
+            for (int i0 = 0; i0 < 32; i0 += 8) {
+                if ((unsigned)i0 <= deg_omega) {
+#pragma unroll
+                    for (int i = i0; i < i0 + 8; ++i) {
+                        if ((unsigned)i <= deg_omega) num1 ^= L.A[pidx(om[i] + e)];
+                        if ((i & 1) == 0 && (unsigned)i <= top) den ^= L.A[pidx(l[i + 1] + e)];
+                        e = addmod(e, rj);
+                    }
+                }
+            }
+            if (den == 0) { count = -1; break; }
+            if (num1 != 0) {
+                const unsigned loc = (rj * c.iprim + 254u) % 255u;
+                if (loc < pad) { count = -1; break; }
+                const unsigned n2 = (unsigned)(((int)rj * ((int)FCR - 1)) % 255 + 255) % 255u;
+                const unsigned cor = L.A[(L.I[num1] + n2 + 255u - L.I[den]) % 255u];
+                unsigned cv = cor, delta = cor;
+                uint8_t *at;
+                if (loc < 255u - NR) {
+                    at = data + (loc - pad);
+                    if (c.dual) {
+                        const unsigned err_dua = *at;
+                        delta = c.into_dual[c.from_dual[err_dua] ^ cor] ^ err_dua;
+                        cv = delta;
+                    }
+                } else {
+                    at = parity + (loc - (255u - NR));
+                    if (c.dual) {
+                        const unsigned err_dua = *at;
+                        delta = c.into_dual[c.from_dual[err_dua] ^ cor] ^ err_dua;
+                    }
+                }
+                *at = (uint8_t)(*at ^ delta);
+                if (corr_out) corr_out[j] = (uint8_t)cv;
+            }
+        }
+    }
+    if (pos_out && count > 0)
+        for (int i = 0; i < count; ++i)
+            pos_out[i] = (L.root[i * 64 + lane] * c.iprim + 254u) % 255u - pad;
+    (void)nroot;
+    return count;
+}
+
+__global__ void __launch_bounds__(64) k_decode_errors(DevCodec c, DecodeArgs a, const uint8_t *syn_ws) {
+    __shared__ __attribute__((aligned(16))) Lds L;
+    const unsigned lane = threadIdx.x;
+    const size_t k0 = (size_t)blockIdx.x * kSpan + 4 * lane;
+    unsigned mine = 0;
+    if (k0 + 4 <= a.ncw && (reinterpret_cast<uintptr_t>(a.result + k0) & 15) == 0) {
+        int4 r;
+        __builtin_memcpy(&r, a.result + k0, 16);
+        mine = (r.x == kSentinel) | (r.y == kSentinel) << 1 | (r.z == kSentinel) << 2 |
+               (r.w == kSentinel) << 3;
+    } else {
+        for (int i = 0; i < 4; ++i)
+            if (k0 + i < a.ncw && a.result[k0 + i] == kSentinel) mine |= 1u << i;
+    }
+    // compact the flagged slots: entry (lane, b) goes to base_b + (lanes below with bit b)
+    unsigned nflag = 0;
+#pragma unroll
+    for (int bit = 0; bit < 4; ++bit) {
+        const uint64_t m = __ballot((mine >> bit) & 1);
+        if ((mine >> bit) & 1) {
+            const unsigned below = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+            L.list[nflag + below] = (uint32_t)(k0 + bit);
+        }
+        nflag += (unsigned)__popcll(m);
+    }
+    if (nflag == 0) return;                       // the common case: a clean span leaves at once
+    for (unsigned i = lane; i < 256; i += 64) {
+        L.A[i] = (uint8_t)c.alpha_to[i];          // alpha_to[255] = 0 (A0)
+        L.I[i] = i == 0 ? (uint16_t)kZ : c.index_of[i];
+    }
+    __syncthreads();
+    for (unsigned c0 = 0; c0 < nflag; c0 += 64) {
+        if (c0 + lane >= nflag) break;
+        const size_t k = L.list[c0 + lane];
+        uint8_t *data = static_cast<uint8_t *>(a.data) + k * a.data_stride;
+        uint8_t *parity = static_cast<uint8_t *>(a.parity) + k * a.parity_stride;
+        const uint32_t *eras = a.eras ? a.eras + k * a.eras_stride : nullptr;
+        const unsigned ne = a.neras ? a.neras[k] : 0;
+        uint32_t *pos = a.positions ? a.positions + k * a.pos_stride : nullptr;
+        uint8_t *corr = a.corr ? static_cast<uint8_t *>(a.corr) + k * a.corr_stride : nullptr;
+        a.result[k] = decode_lane(c, L, lane, data, a.len, parity, eras, ne, pos, corr, syn_ws + k * 32);
+    }
+}
+
+} // namespace
+
+hipError_t launch_decode_flagged(const DevCodec &c, const DecodeArgs &a, const uint8_t *syn_ws,
+                                 hipStream_t s) {
+    if (a.ncw == 0) return hipSuccess;
+    if (c.mm != 8 || c.nroots > 32 || c.masked) return hipErrorInvalidValue;
+    const unsigned grid = (unsigned)((a.ncw + kSpan - 1) / kSpan);
+    hipLaunchKernelGGL(k_decode_errors, dim3(grid), dim3(64), 0, s, c, a, syn_ws);
+    return hipGetLastError();
+}
+
+} // namespace ezrs

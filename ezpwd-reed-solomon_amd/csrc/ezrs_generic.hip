@@ -482,48 +482,6 @@ __global__ void __launch_bounds__(kBlock) k_decode_generic(DevCodec c, DecodeArg
     }
 }
 
-constexpr int32_t kSentinel = INT32_MIN;
-
-// Each thread screens kFlagPer consecutive results (one 16-byte load): a clean batch -- the common
-// case -- costs a quarter of the blocks of a thread-per-codeword screen.
-constexpr int kFlagPer = 4;
-
-constexpr int kFlagBlock = 64;
-
-__global__ void __launch_bounds__(kFlagBlock) k_decode_flagged(DevCodec c, DecodeArgs a,
-                                                               const uint8_t *syn_ws) {
-    __shared__ __attribute__((aligned(16))) uint16_t smem[2 * 256 + 256];
-    __shared__ uint8_t work[kWorkArrays<32> * 33 * kFlagBlock];
-    const size_t k0 = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * kFlagPer;
-    unsigned mine = 0;
-    if (k0 + kFlagPer <= a.ncw && (reinterpret_cast<uintptr_t>(a.result + k0) & 15) == 0) {
-        int4 r;
-        __builtin_memcpy(&r, a.result + k0, 16);
-        mine = (r.x == kSentinel) | (r.y == kSentinel) << 1 | (r.z == kSentinel) << 2 |
-               (r.w == kSentinel) << 3;
-    } else {
-        for (int i = 0; i < kFlagPer; ++i)
-            if (k0 + i < a.ncw && a.result[k0 + i] == kSentinel) mine |= 1u << i;
-    }
-    if (!__syncthreads_or(mine != 0)) return;     // the common case: a clean block leaves at once
-    const uint16_t *A, *I;
-    const uint8_t *ID, *FD;
-    stage_tables<true>(c, smem, A, I, ID, FD);
-    for (int i = 0; i < kFlagPer; ++i) {
-        if (!(mine >> i & 1)) continue;
-        const size_t k = k0 + i;
-        uint8_t *data = static_cast<uint8_t *>(a.data) + k * a.data_stride;
-        uint8_t *parity = static_cast<uint8_t *>(a.parity) + k * a.parity_stride;
-        const uint32_t *eras = a.eras ? a.eras + k * a.eras_stride : nullptr;
-        const unsigned ne = a.neras ? a.neras[k] : 0;
-        uint32_t *pos = a.positions ? a.positions + k * a.pos_stride : nullptr;
-        uint8_t *corr = a.corr ? static_cast<uint8_t *>(a.corr) + k * a.corr_stride : nullptr;
-        a.result[k] = decode_one<uint8_t, 32, kFlagBlock, uint8_t>(c, A, I, ID, FD, data, a.len, parity, eras,
-                                                          ne, pos, corr, syn_ws + k * 32,
-                                                          work + threadIdx.x);
-    }
-}
-
 template <typename T, int MAXR>
 hipError_t enc_launch(const DevCodec &c, const EncodeArgs &a, hipStream_t s) {
     const unsigned grid = (unsigned)((a.ncw + kBlock - 1) / kBlock);
@@ -550,15 +508,6 @@ hipError_t dec_launch(const DevCodec &c, const DecodeArgs &a, hipStream_t s) {
 }
 
 } // namespace
-
-hipError_t launch_decode_flagged(const DevCodec &c, const DecodeArgs &a, const uint8_t *syn_ws,
-                                 hipStream_t s) {
-    if (a.ncw == 0) return hipSuccess;
-    const size_t per = (size_t)kFlagBlock * kFlagPer;
-    const unsigned grid = (unsigned)((a.ncw + per - 1) / per);
-    hipLaunchKernelGGL(k_decode_flagged, dim3(grid), dim3(kFlagBlock), 0, s, c, a, syn_ws);
-    return hipGetLastError();
-}
 
 hipError_t launch_encode_generic(const DevCodec &c, const EncodeArgs &a, hipStream_t s) {
     if (a.ncw == 0) return hipSuccess;

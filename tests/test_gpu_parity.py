@@ -180,15 +180,22 @@ def _inject(torch, cw, n_err, n_era, nn, gen):
     return locs, eras
 
 
-@pytest.mark.parametrize("maker", ["RS(255,223)", "RS_CCSDS(255,223)", "RS(255,251)"])
-def test_bulk_vs_oracle(torch, maker):
-    """64k codewords, random shortened length, error loads 0..3x capacity: every output equals
-    the oracle's (result, positions, corrected data and parity)."""
+# the 17 codecs rsvalidate cross-checks against Karn (rsvalidate.C:46-62), plus CCSDS
+RSVALIDATE_NR = [1, 2, 3, 4, 7, 9, 12, 16, 17, 27, 46, 77, 99, 127, 128, 129, 199]
+BULK = ([("RS(255,223)", 1 << 16), ("RS_CCSDS(255,223)", 1 << 16), ("RS(255,251)", 1 << 16)] +
+        [(f"RS(255,{255 - nr})", 1 << 12) for nr in RSVALIDATE_NR if nr not in (4, 32)])
+
+
+@pytest.mark.parametrize("maker,ncw", BULK)
+def test_bulk_vs_oracle(torch, maker, ncw):
+    """Random shortened length, error loads 0..3x capacity: every output equals the oracle's
+    (result, positions, corrected data and parity); 64k codewords for the headline codecs, 4k for
+    the rest of rsvalidate's set."""
     import ezrs
     c = ezrs.Codec.rs(255, int(maker[7:-1])) if maker.startswith("RS(") else ezrs.Codec.ccsds(223)
     oc = O.Codec(*(O.rs_params(255, c.load) if maker.startswith("RS(") else O.ccsds_params(223)))
     rng = np.random.default_rng(11)
-    ncw, L, nr = 1 << 16, c.load - 17, c.nroots
+    L, nr = c.load - 17, c.nroots
     data = rng.integers(0, 256, (ncw, L + nr)).astype(np.uint8)
     ref = data.copy()
     oc.encode_batch(ref, L, None, nthreads=8)
@@ -197,7 +204,7 @@ def test_bulk_vs_oracle(torch, maker):
     torch.cuda.synchronize()
     np.testing.assert_array_equal(dev.cpu().numpy(), ref)
     # corrupt the oracle's codewords with varying loads
-    load = rng.integers(0, 3 * nr // 2 + 1, ncw)
+    load = rng.integers(0, min(3 * nr // 2, L + nr) + 1, ncw)
     cw = ref.copy()
     eras = np.zeros((ncw, nr), np.uint32)
     neras = np.zeros(ncw, np.uint32)

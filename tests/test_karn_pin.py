@@ -24,6 +24,14 @@ CASES = [("karn_rs255_223", O.rs_params(255, 223)),
          ("karn_ccsds", O.ccsds_params(223, dual=True))]
 
 
+@pytest.fixture(scope="module")
+def torch():
+    import torch as T
+    if not T.cuda.is_available():
+        pytest.skip("no GPU")
+    return T
+
+
 def _load(name):
     return dict(np.load(os.path.join(HERE, "golden", name + ".npz")))
 
