@@ -8,16 +8,22 @@
 // in-place correction and partial fixes kept on failure (1610-1690), positions (1700-1716).
 //
 // Organisation for CDNA4 (m = 8, NR <= 32):
-//  * One wavefront screens 256 result slots (a 16-byte load per lane), compacts the flagged ones into
-//    an LDS list with ballots, and decodes them 64 at a time, one codeword per lane: a sparse batch
-//    keeps every lane busy, a dense one (C3: every codeword flagged) runs at full width.
+//  * A persistent grid of one 16-wave workgroup per CU.  Each wavefront screens spans of 256 result
+//    slots (a 16-byte load per lane), compacts the flagged ones into an LDS list with ballots, and
+//    decodes them 64 at a time, one codeword per lane: a sparse batch keeps every lane busy, a dense
+//    one (C3: every codeword flagged) runs at full width.  A workgroup with nothing flagged leaves
+//    after the screen, before building any table.
 //  * All working polynomials (lambda, B, log lambda, Chien registers, Omega) live in VGPRs: every
 //    loop over coefficients is unrolled, so every index is a constant; coefficient blocks of 8 above
 //    the current degree bound are skipped (deg lambda, deg B <= r - 1 at BM step r).  Only the
 //    syndromes (read at the run-time offset r - 1 - i) and the Chien roots are per-lane LDS arrays.
-//  * GF products through a 256-byte antilog table in LDS (one dword per bank: conflict-free for any
-//    64 indices) with a zero class for log(0): any log >= 510 marks zero, and a product's index is
-//    min(x, x - 255, 255) with alpha_to[255] = 0, so no compare/select per product.
+//  * GF products through a 256-byte antilog table in LDS with a zero class for log(0): any log >= 510
+//    marks zero, and a product's index is min(x, x - 255, 255) with alpha_to[255] = 0, so no
+//    compare/select per product.
+//  * Chien evaluates four consecutive positions per table read: CH[j][x] packs lambda_j-term values
+//    alpha^x, alpha^(x+j), alpha^(x+2j), alpha^(x+3j) into one dword (32 KiB for j = 1..32), so
+//    each register steps by 4j and a zero byte of the XOR marks a root.  That is 64 steps of
+//    deg(lambda) reads instead of 255, the LDS-read rate being what bounds this kernel.
 #include "ezrs_internal.hpp"
 
 namespace ezrs {
@@ -25,8 +31,9 @@ namespace {
 
 constexpr int32_t kSentinel = INT32_MIN;
 constexpr int kSpan = 256;              // result slots screened per wavefront
+constexpr int kWaves = 16;              // wavefronts per workgroup (one workgroup per CU)
 constexpr unsigned kZ = 1024;           // log(0); every value >= 510 is in the zero class
-constexpr int kSrows = 40;              // reversed syndromes: rows 0..31, zero-class padding 32..39
+constexpr int kSrows = 36;              // reversed syndromes: rows 0..31, zero-class padding 32..35
 
 // antilog index of the product of two logs (either may be in the zero class)
 __device__ __forceinline__ unsigned pidx(unsigned x) {
@@ -39,24 +46,30 @@ __device__ __forceinline__ unsigned addmod(unsigned x, unsigned y) {
     return min(s, s - 255u);
 }
 
-struct Lds {
-    uint8_t A[256];                      // alpha_to, A[255] = 0
-    uint16_t I[256];                     // index_of, I[0] = kZ
-    uint32_t list[kSpan];                // flagged codewords of this wave's span
+struct WaveLds {
     uint16_t srev[kSrows * 64];          // [row][lane]: row k holds S_{31-k} (log), rows >= 32 kZ
     uint8_t root[32 * 64];               // [j][lane]: Chien roots in order
+    uint16_t list[kSpan];                // flagged slots of the current span
+};
+struct Lds {
+    uint32_t CH[32 * 256];               // Chien: CH[j-1][x] = alpha^(x + k j), k = 0..3, per byte
+    uint8_t A[256];                      // alpha_to, A[255] = 0
+    uint16_t I[256];                     // index_of, I[0] = kZ
+    WaveLds w[kWaves];
 };
 
-__device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, Lds &L, const unsigned lane, uint8_t *data, unsigned len,
-                           uint8_t *parity, const uint32_t *eras, unsigned no_eras, uint32_t *pos_out,
-                           uint8_t *corr_out, const uint8_t *syn_in) {
+__device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, const Lds &L, WaveLds &W,
+                                                          const unsigned lane, uint8_t *data, unsigned len,
+                                                          uint8_t *parity, const uint32_t *eras,
+                                                          unsigned no_eras, uint32_t *pos_out,
+                                                          uint8_t *corr_out, const uint8_t *syn_in) {
     const unsigned NR = c.nroots, LOAD = c.load, FCR = c.fcr, PRM = c.prim;
     if (len == 0 || len > LOAD) return -1;                                    // 1375-1377
     if (no_eras > NR) return -1;                                              // 1380-1382
     for (unsigned i = 0; i < no_eras; ++i)
         if (eras[i] >= len + NR) return -1;                                   // 1383-1387
     const unsigned pad = LOAD - len;
-    auto S = [&](int k) -> uint16_t & { return L.srev[k * 64 + lane]; };
+    auto S = [&](int k) -> uint16_t & { return W.srev[k * 64 + lane]; };
 
     // syndromes (polynomial form from the syndrome kernel) -> logs, stored reversed (1416-1434)
     unsigned syn_error = 0;
@@ -84,12 +97,12 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, Lds
         lam[1] = L.A[(PRM * (c.nn - 1 - (eras[0] + pad))) % 255u];
         for (unsigned e = 1; e < no_eras; ++e) {
             const unsigned u = (PRM * (c.nn - 1 - (eras[e] + pad))) % 255u;
-            // lam[j] ^= lam[j-1] * alpha^u for j = e+1 .. 1 (lam[j-1] == 0 above j - 1 > e)
+            // lam[j] ^= lam[j-1] * alpha^u for j = e+1 .. 1 (lam[j-1] == 0 for j - 1 > e)
 #pragma unroll
-            for (int j0 = 32; j0 >= 0; j0 -= 8) {
+            for (int j0 = 32; j0 >= 0; j0 -= 4) {
                 if ((unsigned)(j0 > 0 ? j0 - 1 : 0) <= e) {
 #pragma unroll
-                    for (int j = j0 + 7; j >= j0; --j) {
+                    for (int j = j0 + 3; j >= j0; --j) {
                         if (j < 1 || j > 32) continue;
                         lam[j] ^= L.A[pidx(u + L.I[lam[j - 1]])];
                     }
@@ -101,16 +114,17 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, Lds
 #pragma unroll
     for (int i = 0; i <= 32; ++i) b[i] = i == 0 ? 0u : L.I[lam[i]];
 
-    // Berlekamp-Massey (1507-1546).  At step r, lambda and B have degree <= r - 1.
+    // Berlekamp-Massey (1507-1546).  At step r, lambda and B have degree <= r - 1, so blocks of 4
+    // coefficients starting above r hold zeros and are skipped.
     unsigned el = no_eras;
     for (unsigned r = no_eras + 1; r <= NR; ++r) {
         const int sb = 32 - (int)r;           // row of S_{r-1}; S_{r-1-i} at row sb + i
         unsigned discr = 0;
 #pragma unroll
-        for (int i0 = 0; i0 <= 32; i0 += 8) {
+        for (int i0 = 0; i0 <= 32; i0 += 4) {
             if ((unsigned)i0 <= r) {
 #pragma unroll
-                for (int i = i0; i < i0 + 8 && i <= 32; ++i) {
+                for (int i = i0; i < i0 + 4 && i <= 32; ++i) {
                     l[i] = i == 0 ? 0u : L.I[lam[i]];
                     if (i < 32) discr ^= L.A[pidx(l[i] + S(sb + i))];
                 }
@@ -120,10 +134,10 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, Lds
         const bool upd = dl < 510u && 2 * el <= r + no_eras - 1;
         const unsigned ndl = 255u - dl;
 #pragma unroll
-        for (int i0 = 32; i0 >= 0; i0 -= 8) {
+        for (int i0 = 32; i0 >= 0; i0 -= 4) {
             if ((unsigned)i0 <= r) {
 #pragma unroll
-                for (int i = i0 + 7; i >= i0; --i) {
+                for (int i = i0 + 3; i >= i0; --i) {
                     if (i > 32) continue;
                     const unsigned bp = i > 0 ? b[i - 1] : kZ;
                     if (i > 0) lam[i] ^= L.A[pidx(dl + bp)];
@@ -144,31 +158,40 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, Lds
         if (i > 0 && lam[i] != 0) deg = i;
     }
 
-    // Chien search (1555-1584): registers reg_j = log lambda_j + j*i (mod 255), roots in order
+    // Chien search (1555-1584), four positions i .. i+3 per step: rg[j] = 4 * ((log lambda_j +
+    // j*i) mod 255) addresses CH[j-1]; lambda_j = 0 keeps rg in the zero class (clamped to entry 255)
     int count = 0;
     if (deg > 0) {
         unsigned rg[33];
 #pragma unroll
-        for (int j = 1; j <= 32; ++j) rg[j] = l[j] < 255u ? l[j] : 0x80000000u;
-        for (unsigned i = 1; i <= 255; ++i) {
-            unsigned q = 1;
+        for (int j = 1; j <= 32; ++j) rg[j] = l[j] < 255u ? 4u * addmod(l[j], (unsigned)j) : 0x80000000u;
+        for (unsigned i = 1; i <= 255; i += 4) {
+            unsigned q = 0x01010101u;
 #pragma unroll
-            for (int j0 = 1; j0 <= 32; j0 += 8) {
+            for (int j0 = 1; j0 <= 32; j0 += 4) {
                 if ((unsigned)j0 <= deg) {
 #pragma unroll
-                    for (int j = j0; j < j0 + 8; ++j) {
-                        const unsigned a = rg[j] + j, z = rg[j] + (j - 255u);
+                    for (int j = j0; j < j0 + 4; ++j) {
+                        q ^= *reinterpret_cast<const uint32_t *>(
+                            reinterpret_cast<const uint8_t *>(L.CH + (j - 1) * 256) + min(rg[j], 1020u));
+                        const unsigned a = rg[j] + 16u * j, z = a - 1020u;
                         rg[j] = min(a, z);
-                        q ^= L.A[min(rg[j], 255u)];
                     }
                 }
             }
-            if (q != 0) continue;
-            L.root[count * 64 + lane] = (uint8_t)i;
-            if (++count == (int)deg) break;
+            if (i == 253) q |= 0xff000000u;                     // position 256 does not exist
+            if (((q - 0x01010101u) & ~q & 0x80808080u) == 0) continue;
+            bool done = false;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (((q >> (8 * k)) & 255u) == 0) {
+                    W.root[count * 64 + lane] = (uint8_t)(i + k);
+                    if (++count == (int)deg) { done = true; break; }
+                }
+            }
+            if (done) break;
         }
     }
-    const int nroot = count;
     if ((int)deg != count || deg == 0) count = -1;                           // 1577-1595
 
     if (count > 0) {
@@ -176,10 +199,10 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, Lds
         const unsigned deg_omega = deg - 1;
         unsigned om[32];
 #pragma unroll
-        for (int i0 = 0; i0 < 32; i0 += 8) {
+        for (int i0 = 0; i0 < 32; i0 += 4) {
             if ((unsigned)i0 <= deg_omega) {
 #pragma unroll
-                for (int i = i0; i < i0 + 8; ++i) {
+                for (int i = i0; i < i0 + 4; ++i) {
                     unsigned t = 0;
 #pragma unroll
                     for (int j = 0; j <= i; ++j) t ^= L.A[pidx(S(31 - (i - j)) + l[j])];
@@ -190,13 +213,13 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, Lds
         const unsigned top = (deg < NR - 1 ? deg : NR - 1) & ~1u;
         // Forney, roots in reverse order, corrections applied as found (1610-1690)
         for (int j = count - 1; j >= 0; --j) {
-            const unsigned rj = L.root[j * 64 + lane];
+            const unsigned rj = W.root[j * 64 + lane];
             unsigned num1 = 0, den = 0, e = 0;     // e = i * rj (mod 255)
 #pragma unroll
-            for (int i0 = 0; i0 < 32; i0 += 8) {
+            for (int i0 = 0; i0 < 32; i0 += 4) {
                 if ((unsigned)i0 <= deg_omega) {
 #pragma unroll
-                    for (int i = i0; i < i0 + 8; ++i) {
+                    for (int i = i0; i < i0 + 4; ++i) {
                         if ((unsigned)i <= deg_omega) num1 ^= L.A[pidx(om[i] + e)];
                         if ((i & 1) == 0 && (unsigned)i <= top) den ^= L.A[pidx(l[i + 1] + e)];
                         e = addmod(e, rj);
@@ -232,15 +255,13 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, Lds
     }
     if (pos_out && count > 0)
         for (int i = 0; i < count; ++i)
-            pos_out[i] = (L.root[i * 64 + lane] * c.iprim + 254u) % 255u - pad;
-    (void)nroot;
+            pos_out[i] = (W.root[i * 64 + lane] * c.iprim + 254u) % 255u - pad;
     return count;
 }
 
-__global__ void __launch_bounds__(64) k_decode_errors(DevCodec c, DecodeArgs a, const uint8_t *syn_ws) {
-    __shared__ __attribute__((aligned(16))) Lds L;
-    const unsigned lane = threadIdx.x;
-    const size_t k0 = (size_t)blockIdx.x * kSpan + 4 * lane;
+// Screen span `sp`: the flagged slots' offsets into `list` (when given), their number returned.
+__device__ __forceinline__ unsigned screen(const DecodeArgs &a, size_t sp, unsigned lane, uint16_t *list) {
+    const size_t k0 = sp * kSpan + 4 * lane;
     unsigned mine = 0;
     if (k0 + 4 <= a.ncw && (reinterpret_cast<uintptr_t>(a.result + k0) & 15) == 0) {
         int4 r;
@@ -251,34 +272,62 @@ __global__ void __launch_bounds__(64) k_decode_errors(DevCodec c, DecodeArgs a, 
         for (int i = 0; i < 4; ++i)
             if (k0 + i < a.ncw && a.result[k0 + i] == kSentinel) mine |= 1u << i;
     }
-    // compact the flagged slots: entry (lane, b) goes to base_b + (lanes below with bit b)
+    // entry (lane, bit) goes to base_bit + (lanes below with that bit)
     unsigned nflag = 0;
 #pragma unroll
     for (int bit = 0; bit < 4; ++bit) {
         const uint64_t m = __ballot((mine >> bit) & 1);
-        if ((mine >> bit) & 1) {
+        if (list && ((mine >> bit) & 1)) {
             const unsigned below = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
                                                              __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-            L.list[nflag + below] = (uint32_t)(k0 + bit);
+            list[nflag + below] = (uint16_t)(4 * lane + bit);
         }
         nflag += (unsigned)__popcll(m);
     }
-    if (nflag == 0) return;                       // the common case: a clean span leaves at once
-    for (unsigned i = lane; i < 256; i += 64) {
+    return nflag;
+}
+
+__global__ void __launch_bounds__(64 * kWaves) k_decode_errors(DevCodec c, DecodeArgs a, const uint8_t *syn_ws) {
+    __shared__ __attribute__((aligned(16))) Lds L;
+    const unsigned lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const size_t nspan = (a.ncw + kSpan - 1) / kSpan, step = (size_t)gridDim.x * kWaves;
+    unsigned any = 0;
+    for (size_t sp = (size_t)blockIdx.x * kWaves + wave; sp < nspan; sp += step)
+        any |= screen(a, sp, lane, nullptr);
+    if (!__syncthreads_or(any != 0)) return;      // the common case: nothing flagged here
+
+    for (unsigned i = threadIdx.x; i < 256; i += 64 * kWaves) {
         L.A[i] = (uint8_t)c.alpha_to[i];          // alpha_to[255] = 0 (A0)
         L.I[i] = i == 0 ? (uint16_t)kZ : c.index_of[i];
     }
     __syncthreads();
-    for (unsigned c0 = 0; c0 < nflag; c0 += 64) {
-        if (c0 + lane >= nflag) break;
-        const size_t k = L.list[c0 + lane];
-        uint8_t *data = static_cast<uint8_t *>(a.data) + k * a.data_stride;
-        uint8_t *parity = static_cast<uint8_t *>(a.parity) + k * a.parity_stride;
-        const uint32_t *eras = a.eras ? a.eras + k * a.eras_stride : nullptr;
-        const unsigned ne = a.neras ? a.neras[k] : 0;
-        uint32_t *pos = a.positions ? a.positions + k * a.pos_stride : nullptr;
-        uint8_t *corr = a.corr ? static_cast<uint8_t *>(a.corr) + k * a.corr_stride : nullptr;
-        a.result[k] = decode_lane(c, L, lane, data, a.len, parity, eras, ne, pos, corr, syn_ws + k * 32);
+    for (unsigned t = threadIdx.x; t < 32 * 256; t += 64 * kWaves) {
+        const unsigned j = t / 256 + 1, x = t % 256;
+        uint32_t v = 0;
+        if (x < 255)
+            for (unsigned k = 0; k < 4; ++k) v |= (uint32_t)L.A[(x + k * j) % 255u] << (8 * k);
+        L.CH[t] = v;
+    }
+    __syncthreads();
+
+    WaveLds &W = L.w[wave];
+    for (size_t sp = (size_t)blockIdx.x * kWaves + wave; sp < nspan; sp += step) {
+        const unsigned n = screen(a, sp, lane, W.list);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // list entries of other lanes
+        for (unsigned c0 = 0; c0 < n; c0 += 64) {
+            if (c0 + lane < n) {
+                const size_t k = sp * kSpan + W.list[c0 + lane];
+                uint8_t *data = static_cast<uint8_t *>(a.data) + k * a.data_stride;
+                uint8_t *parity = static_cast<uint8_t *>(a.parity) + k * a.parity_stride;
+                const uint32_t *eras = a.eras ? a.eras + k * a.eras_stride : nullptr;
+                const unsigned ne = a.neras ? a.neras[k] : 0;
+                uint32_t *pos = a.positions ? a.positions + k * a.pos_stride : nullptr;
+                uint8_t *corr = a.corr ? static_cast<uint8_t *>(a.corr) + k * a.corr_stride : nullptr;
+                a.result[k] = decode_lane(c, L, W, lane, data, a.len, parity, eras, ne, pos, corr,
+                                          syn_ws + k * 32);
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // list reads done before the next span
     }
 }
 
@@ -288,8 +337,10 @@ hipError_t launch_decode_flagged(const DevCodec &c, const DecodeArgs &a, const u
                                  hipStream_t s) {
     if (a.ncw == 0) return hipSuccess;
     if (c.mm != 8 || c.nroots > 32 || c.masked) return hipErrorInvalidValue;
-    const unsigned grid = (unsigned)((a.ncw + kSpan - 1) / kSpan);
-    hipLaunchKernelGGL(k_decode_errors, dim3(grid), dim3(64), 0, s, c, a, syn_ws);
+    const size_t nspan = (a.ncw + kSpan - 1) / kSpan;
+    const size_t want = (nspan + kWaves - 1) / kWaves;
+    const unsigned grid = (unsigned)(want < (size_t)c.ncu ? want : (size_t)c.ncu);
+    hipLaunchKernelGGL(k_decode_errors, dim3(grid), dim3(64 * kWaves), 0, s, c, a, syn_ws);
     return hipGetLastError();
 }
 
