@@ -16,6 +16,8 @@ run() {  # name timeout cmd...
 run pytest 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
 run smoke 240 python -c "import __graft_entry__ as g; g.smoke()"
 run bench_c2 400 python bench.py --steps 20 --warmup 3 --e2e
+run bench_c1 300 python bench.py --workload c1 --steps 20 --warmup 3
+run bench_shards 400 python bench.py --workload shards --steps 10 --warmup 2 --no-cpu-baseline
 run bench_c3 400 python bench.py --workload c3 --steps 10 --warmup 2
 run bench_c4 400 python bench.py --workload c4 --steps 3 --warmup 1
 run bench_c5 400 python bench.py --workload c5 --steps 20 --warmup 3
