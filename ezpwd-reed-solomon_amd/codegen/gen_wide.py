@@ -1,0 +1,218 @@
+#!/usr/bin/env python3
+"""Generate gen/ezrs_wide_tables.inc: the GF(2)-linear remainder networks of the GF(2^16) syndrome
+kernels (ezrs_wide.hip).
+
+Derivation.  The syndromes of decode_symbols (c++/ezpwd/rs_base:1390-1414) are
+S_i = r(beta_i), beta_i = alpha^(e_i), e_i = (fcr + i) * prim mod NN, with r(x) the received word
+(data[0] the highest-degree coefficient).  Let M_e(x) be the minimal polynomial of alpha^e over
+GF(2) (binary coefficients, degree 16 for every e that occurs here) and R_e = r mod M_e.  Then
+r(beta) = R_e(beta) for every conjugate beta = alpha^(e 2^k), so one remainder per cyclotomic coset
+("leader") serves all the syndromes of that coset.  Because M_e is binary, R_e is computed with
+XORs of whole 16-bit symbols only: a GF(2)-linear shift register whose taps are the 1-bits of M_e.
+
+Blocks of 16 symbols c_0..c_15 (c_0 first) update the 16 remainder words s[0..15]
+(R = sum_k s[k] x^k) as
+    R' = R x^16 + sum_t c_t x^(15-t)  (mod M_e)
+and the input terms need no reduction (degree < 16), so
+    s'[k] = c[15-k]  XOR  XOR_{i : bit k of (x^(16+i) mod M_e)} s[i].
+Each s'[k] is emitted as a chain of v_bitop3 three-input XORs after a greedy common-pair
+elimination across the 16 rows (pairs shared by >= 2 rows are formed once).
+
+A 32-bit word packs the same position of two codewords (low half: even codeword of the lane's
+pair, high half: odd), so every XOR advances two codewords.
+
+Run from the repo root: python3 ezpwd-reed-solomon_amd/codegen/gen_wide.py
+"""
+import os
+import sys
+
+# (m, poly, fcr, prim, nroots): the GF(2^16) codecs with a fast path.  RS<65535,65503> is BASELINE
+# config C4 (rs:47-104 maps RS<N,K> to poly 0x1100b, fcr 1, prim 1).
+CODECS = [
+    (16, 0x1100B, 1, 1, 32),
+    (16, 0x1100B, 1, 1, 16),
+]
+
+
+class GF:
+    def __init__(self, m, poly):
+        self.m, self.nn = m, (1 << m) - 1
+        self.exp = [0] * (2 * self.nn)
+        self.log = [0] * (self.nn + 1)
+        x = 1
+        for i in range(self.nn):
+            self.exp[i] = self.exp[i + self.nn] = x
+            self.log[x] = i
+            x <<= 1
+            if x >> m:
+                x ^= poly
+        assert x == 1
+
+    def mul(self, a, b):
+        if not a or not b:
+            return 0
+        return self.exp[self.log[a] + self.log[b]]
+
+
+def min_poly(gf, e):
+    """Binary minimal polynomial of alpha^e as an int (bit k = coefficient of x^k)."""
+    conj, x = [], e % gf.nn
+    while x not in conj:
+        conj.append(x)
+        x = 2 * x % gf.nn
+    p = [1]                                   # coefficients, low to high, in GF(2^m)
+    for c in conj:
+        r = gf.exp[c]
+        q = [0] * (len(p) + 1)
+        for k, a in enumerate(p):             # p * (x + r)
+            q[k + 1] ^= a
+            q[k] ^= gf.mul(a, r)
+        p = q
+    assert all(a in (0, 1) for a in p), "minimal polynomial not binary"
+    return sum(a << k for k, a in enumerate(p)), len(conj)
+
+
+def leaders(m, poly, fcr, prim, nr):
+    gf = GF(m, poly)
+    seen, lead, syn_leader = {}, [], []
+    for i in range(nr):
+        e = (fcr + i) * prim % gf.nn
+        c, x = [], e
+        while x not in c:
+            c.append(x)
+            x = 2 * x % gf.nn
+        ld = min(c)
+        if ld not in seen:
+            seen[ld] = len(lead)
+            lead.append(ld)
+        syn_leader.append(seen[ld])
+    return gf, lead, syn_leader
+
+
+def block_rows(mp, d):
+    """rows[k] = the state indices i whose x^(d+i) mod M has bit k set."""
+    def reduce(v):
+        for b in range(v.bit_length() - 1, d - 1, -1):
+            if v >> b & 1:
+                v ^= mp << (b - d)
+        return v
+    cols = [reduce(1 << (d + i)) for i in range(d)]
+    return [[i for i in range(d) if cols[i] >> k & 1] for k in range(d)]
+
+
+def cse(rows):
+    """Greedy common-pair elimination.  Returns (temps, rows) with temps = [(name, a, b)]."""
+    rows = [list(r) for r in rows]
+    temps = []
+    while True:
+        cnt = {}
+        for r in rows:
+            rs = sorted(r, key=str)
+            for x in range(len(rs)):
+                for y in range(x + 1, len(rs)):
+                    k = (rs[x], rs[y])
+                    cnt[k] = cnt.get(k, 0) + 1
+        if not cnt:
+            break
+        (a, b), n = max(cnt.items(), key=lambda kv: (kv[1], str(kv[0])))
+        if n < 2:
+            break
+        t = f"t{len(temps)}"
+        temps.append((t, a, b))
+        for r in rows:
+            if a in r and b in r:
+                r.remove(a)
+                r.remove(b)
+                r.append(t)
+    return temps, rows
+
+
+def term(x):
+    return f"s{x}" if isinstance(x, int) else x
+
+
+def xor_chain(terms):
+    terms = list(terms)
+    acc, rest = terms[0], terms[1:]
+    while rest:
+        if len(rest) >= 2:
+            acc, rest = f"xor3({acc}, {rest[0]}, {rest[1]})", rest[2:]
+        else:
+            acc, rest = f"({acc} ^ {rest[0]})", rest[1:]
+    return acc
+
+
+def gen_block(name, mp, d):
+    rows = block_rows(mp, d)
+    temps, rows = cse(rows)
+    ops = 0
+    out = [f"__device__ __forceinline__ void {name}(uint32_t (&s)[{d}], const uint32_t (&c)[{d}]) {{"]
+    out += [f"    const uint32_t s{i} = s[{i}];" for i in range(d)]
+    for t, a, b in temps:
+        out.append(f"    const uint32_t {t} = {term(a)} ^ {term(b)};")
+        ops += 1
+    for k in range(d):
+        terms = [f"c[{d - 1 - k}]"] + [term(x) for x in rows[k]]
+        out.append(f"    s[{k}] = {xor_chain(terms)};")
+        ops += (len(terms) - 1 + 1) // 2
+    out.append("}")
+    return out, ops
+
+
+def gen_codec(m, poly, fcr, prim, nr):
+    gf, lead, syn_leader = leaders(m, poly, fcr, prim, nr)
+    tag = f"RS_{gf.nn}_{gf.nn - nr}" if (poly, fcr, prim) == (0x1100B, 1, 1) else \
+        f"C{m}_{poly:x}_{fcr}_{prim}_{nr}"
+    out = [f"// ---- {tag}: m={m} poly={poly:#x} fcr={fcr} prim={prim} nroots={nr}: "
+           f"{len(lead)} coset leaders ----"]
+    costs = []
+    for li, e in enumerate(lead):
+        mp, d = min_poly(gf, e)
+        assert d == m, f"leader {e}: degree {d}"
+        body, ops = gen_block(f"wb_{tag}_{li}", mp, d)
+        costs.append(ops)
+        out.append(f"// leader {e}: M(x) = {mp:#x}, {ops} ops per 16-symbol block")
+        out += body
+    nl = len(lead)
+    out.append(f"struct WC_{tag} {{")
+    out.append(f"    static constexpr unsigned M = {m}, POLY = {poly:#x}, FCR = {fcr}, PRIM = {prim}, NR = {nr};")
+    out.append(f"    static constexpr int NL = {nl};")
+    out.append("    template <int L>")
+    out.append("    static __device__ __forceinline__ void block(uint32_t (&s)[16], const uint32_t (&c)[16]) {")
+    for li in range(nl):
+        kw = "if" if li == 0 else "else if"
+        out.append(f"        {kw} constexpr (L == {li}) wb_{tag}_{li}(s, c);")
+    out.append("    }")
+    out.append("};")
+    out.append(f"// total {sum(costs)} ops per 16 symbols x 2 codewords "
+               f"({sum(costs) / 32:.2f} per codeword-symbol)")
+    return tag, out
+
+
+def main():
+    here = os.path.dirname(os.path.abspath(__file__))
+    dst = os.path.join(here, "..", "csrc", "gen", "ezrs_wide_tables.inc")
+    body = ["// Generated by codegen/gen_wide.py -- do not edit.",
+            "#pragma once",
+            "namespace ezrs {",
+            "namespace wide {",
+            "__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {",
+            "    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);",
+            "}"]
+    tags = []
+    for cd in CODECS:
+        tag, out = gen_codec(*cd)
+        tags.append(tag)
+        body += out
+    body.append("#define EZRS_WIDE_CODEC_LIST(X) \\")
+    cont = " \\"
+    body += [f"    X({t})" + (cont if i + 1 < len(tags) else "") for i, t in enumerate(tags)]
+    body += ["} // namespace wide", "} // namespace ezrs", ""]
+    with open(dst, "w") as f:
+        f.write("\n".join(body))
+    if "-v" in sys.argv:
+        print("\n".join(l for l in body if l.startswith("//")))
+
+
+if __name__ == "__main__":
+    main()

@@ -33,6 +33,9 @@ struct ezrs_codec {
     hipStream_t streams[2] = {nullptr, nullptr};
     int bs_id = -1;               // bit-sliced GF(2^8) kernel set, -1 if none
     int ps_id = -1;               // plane-sliced GF(2^8) kernel set, -1 if none
+    int wide_id = -1;             // GF(2^16) remainder kernel set, -1 if none
+    std::vector<uint16_t> wide_blob;   // host: leader slots | log beta | log Q
+    uint16_t *d_qlog = nullptr;   // device copy of log Q
     // Device workspaces of the batch entry points, one per HIP stream: calls on different streams
     // never share scratch memory, calls on one stream are ordered by the stream.  A workspace only
     // grows; the buffer it replaces is kept until ezrs_destroy, so work already queued (or a
@@ -159,6 +162,22 @@ int ezrs_create(ezrs_codec **out, unsigned symbol_bits, unsigned poly, unsigned 
     // EZRS_NO_PLANESLICE=1 keeps the per-symbol bit-sliced kernels (A/B measurements)
     const char *nops = getenv("EZRS_NO_PLANESLICE");
     c->ps_id = (nops && *nops == '1') ? -1 : planeslice_codec_id(d);
+    // EZRS_NO_WIDE=1 keeps the lane-group GF(2^16) kernels (A/B measurements)
+    const char *now = getenv("EZRS_NO_WIDE");
+    c->wide_id = (now && *now == '1') ? -1 : wide_codec_id(d);
+    if (c->wide_id >= 0) {
+        if (!wide_build_consts(c->wide_id, m, c->wide_blob)) {
+            c->wide_id = -1;
+        } else {
+            const size_t qn = (size_t)m.spec.nroots * m.spec.nroots;
+            if ((e = hipMalloc(&c->d_qlog, qn * sizeof(uint16_t))) != hipSuccess ||
+                (e = hipMemcpy(c->d_qlog, c->wide_blob.data() + 64, qn * sizeof(uint16_t),
+                               hipMemcpyHostToDevice)) != hipSuccess) {
+                ezrs_destroy(c);
+                return hip_fail(e, "hipMalloc(wide tables)");
+            }
+        }
+    }
     *out = c;
     return 0;
 }
@@ -188,6 +207,7 @@ int ezrs_destroy(ezrs_codec *c) {
     DeviceGuard g(c->device);
     (void)hipFree(c->d_tabs);
     (void)hipFree(c->d_dual);
+    if (c->d_qlog) (void)hipFree(c->d_qlog);
     for (auto &kv : c->ws) (void)hipFree(kv.second.p);
     for (void *p : c->ws_retired) (void)hipFree(p);
     for (int i = 0; i < 2; ++i) {
@@ -222,6 +242,7 @@ size_t ws_bytes_for(const ezrs_codec *c, size_t ncw) {
     size_t b = 0;                                          // both >= ncw * 32 (decode's need)
     if (c->bs_id >= 0) b = bs_encode_ws_bytes(ncw);
     if (c->ps_id >= 0 && ps_ws_bytes(ncw) > b) b = ps_ws_bytes(ncw);
+    if (c->wide_id >= 0 && wide_ws_bytes(c->wide_id, ncw) > b) b = wide_ws_bytes(c->wide_id, ncw);
     return b;
 }
 
@@ -251,6 +272,8 @@ namespace {
 // ws: bs_encode_ws_bytes(ncw) bytes (bit-sliced path only).
 hipError_t dispatch_encode(const ezrs_codec *c, const EncodeArgs &a, void *ws, hipStream_t st) {
     if (c->ps_id >= 0 && ps_can_encode(c->dev, a)) return launch_ps_encode(c->ps_id, c->dev, a, ws, st);
+    if (c->wide_id >= 0 && wide_can_encode(c->dev, a))
+        return launch_wide_encode(c->wide_id, c->dev, a, c->wide_blob.data(), c->d_qlog, ws, st);
     return c->bs_id >= 0 ? launch_bs_encode(c->bs_id, c->dev, a, ws, st) : launch_encode_generic(c->dev, a, st);
 }
 
@@ -265,6 +288,8 @@ hipError_t dispatch_decode(const ezrs_codec *c, const DecodeArgs &a, uint8_t *sy
         if (e == hipSuccess) e = launch_decode_flagged(c->dev, a, syn_ws, st);
         return e;
     }
+    if (c->wide_id >= 0 && wide_can_decode(c->dev, a))
+        return launch_wide_decode(c->wide_id, c->dev, a, c->wide_blob.data(), c->d_qlog, syn_ws, st);
     if (c->bs_id >= 0 && contiguous) {
         // Bit-sliced syndromes for the whole batch; the reference algorithm only for the codewords
         // that are not valid as received (or carry erasures to validate).

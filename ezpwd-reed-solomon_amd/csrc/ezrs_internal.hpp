@@ -7,6 +7,7 @@
 #include <cstdint>
 #include <mutex>
 #include <type_traits>
+#include <vector>
 
 #include "ezrs_field.hpp"
 
@@ -86,5 +87,19 @@ bool ps_can_decode(const DevCodec &d, const DecodeArgs &a);
 hipError_t launch_ps_encode(int id, const DevCodec &d, const EncodeArgs &a, void *ws, hipStream_t s);
 hipError_t launch_ps_syndromes(int id, const DevCodec &d, const DecodeArgs &a, uint8_t *syn_ws,
                                hipStream_t s);
+
+// GF(2^16) kernels (ezrs_wide.hip) for the codecs of gen/ezrs_wide_tables.inc: remainder networks
+// + syndrome/parity finish + wavefront-per-codeword error path.  Decode needs inline parity.
+int wide_codec_id(const DevCodec &d);        // -1 if the codec has no wide fast path
+size_t wide_ws_bytes(int id, size_t ncw);
+// blob: syndrome leader slots [32] | log beta [32] | log Q [NR][NR] (host copy; the Q part is
+// also uploaded to the device)
+bool wide_build_consts(int id, const CodecMath &m, std::vector<uint16_t> &blob);
+bool wide_can_encode(const DevCodec &d, const EncodeArgs &a);
+bool wide_can_decode(const DevCodec &d, const DecodeArgs &a);
+hipError_t launch_wide_encode(int id, const DevCodec &d, const EncodeArgs &a, const uint16_t *blob_host,
+                              const uint16_t *qlog_dev, void *ws, hipStream_t s);
+hipError_t launch_wide_decode(int id, const DevCodec &d, const DecodeArgs &a, const uint16_t *blob_host,
+                              const uint16_t *qlog_dev, void *ws, hipStream_t s);
 
 } // namespace ezrs

@@ -1,0 +1,697 @@
+// ezrs_wide.hip -- GF(2^16) RS fast path (BASELINE config C4: RS(65535,65503)).
+//
+// Syndromes S_i = r(beta_i) (c++/ezpwd/rs_base:1390-1414) through binary minimal polynomials:
+// for each cyclotomic coset ("leader" e) of the roots, R_e = r mod M_e(x) is a GF(2)-linear shift
+// register over whole 16-bit symbols (XOR only; codegen/gen_wide.py has the derivation), and every
+// root beta of the coset gives S = R_e(beta), 16 GF(2^16) products per syndrome.
+//
+//   k_wide_rem     streams 128-codeword tiles through LDS (LDS-DMA, 128-symbol windows, double
+//                  buffered); wave w runs the networks of leaders 2w, 2w+1 on 32-bit words that pack
+//                  one position of two codewords.  Out: remainders [ncw][NLP][16] u16.
+//   k_wide_finish  32 lanes per codeword evaluate the syndromes.  Encode: parity = Q S with
+//                  Q = V^-1 diag(beta^NR) (V[i][k] = beta_i^(NR-1-k)), the unique parity whose
+//                  codeword has zero syndromes -- encode_symbols' LFSR result (rs_base:1296-1332).
+//                  Decode: result 0 for a codeword with zero syndromes and no erasures
+//                  (rs_base:1416-1434); the others get queued for
+//   k_wide_errors  one wavefront per flagged codeword: erasure locator + Berlekamp-Massey with the
+//                  discrepancy as a wave reduction (rs_base:1436-1546), Chien search over all NN
+//                  positions spread over the 64 lanes with alpha_to in LDS, roots kept in the
+//                  reference's ascending order by ballot + prefix count (1548-1584), Omega and
+//                  Forney per root lane (1589-1690), the reference's partial-correction-on-failure
+//                  semantics, positions in the pad-relative frame (1713-1716).
+#include "ezrs_internal.hpp"
+#include "gen/ezrs_wide_tables.inc"
+
+namespace ezrs {
+namespace wide {
+
+constexpr int kRows = 128;                  // codewords per tile (64 pairs)
+constexpr int kWin = 128;                   // symbols per window
+constexpr int kRowBytes = 2 * kWin;         // 256 B of each row per window
+constexpr int kBuf = kRows * kRowBytes;     // 32 KiB
+constexpr int kLPW = 2;                     // leaders per wave
+constexpr int kMaxNR = 32;
+constexpr int32_t kSentinel = INT32_MIN;
+
+typedef int rsrc_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+
+// Buffer descriptor of [base, base + span): raw, out-of-range bytes read as zero.
+__device__ __forceinline__ rsrc_t make_rsrc(const uint8_t *base, uint32_t span) {
+    const uint64_t p = (uint64_t)(uintptr_t)base;
+    rsrc_t r;
+    r.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)p);
+    r.y = __builtin_amdgcn_readfirstlane((int)((uint32_t)(p >> 32) & 0xFFFFu));
+    r.z = __builtin_amdgcn_readfirstlane((int)span);
+    r.w = 0x00020000;
+    return r;
+}
+
+struct RemArgs {
+    const uint8_t *base;        // row 0 of the batch
+    size_t stride;              // row pitch, bytes
+    uint32_t n;                 // symbols evaluated from each row's start
+    uint32_t ncw;
+    uint16_t *rem;              // [ncw][nlp][16]
+    uint32_t nlp;               // leaders padded to the waves (NW * kLPW)
+};
+
+// LDS image of one window: row r (pair p = r >> 1) at r * 256; its 16-byte chunk c = 2b + h
+// (b = 16-symbol block) at slot 2 (b ^ (p & 7)) + (h ^ q), q = (p >> 3) & 1.  Each 16-lane group
+// of a ds_read_b128 holds 16 distinct p mod 16 and so reads 16 distinct bank quads.
+template <class C, int W>
+__device__ __forceinline__ void rem_body(const RemArgs &a, uint8_t *lds, int lane) {
+    constexpr int NW = (C::NL + kLPW - 1) / kLPW;
+    const size_t row0 = (size_t)blockIdx.x * kRows;
+    const uint32_t rows = a.ncw - row0 < (size_t)kRows ? (uint32_t)(a.ncw - row0) : (uint32_t)kRows;
+    const uint8_t *tbase = a.base + row0 * a.stride;
+    const uint32_t span = (uint32_t)((rows - 1) * a.stride + 2u * a.n);
+    const rsrc_t rsrc = make_rsrc(tbase, span);
+    const uint32_t nwin = (a.n + kWin - 1) / kWin;
+    const uint32_t z = nwin * kWin - a.n;             // leading positions of window 0 to ignore
+    const uint32_t lbuf = __builtin_amdgcn_readfirstlane(lds_addr(lds));
+    const uint32_t stride = (uint32_t)a.stride;
+
+    // DMA role: instructions i = W, W + NW, ... < 32; instruction i covers rows 4i .. 4i + 3, lane j
+    // -> row 4i + j / 16, slot j % 16.
+    auto issue = [&](uint32_t w, uint32_t buf) {
+        uint32_t l = (uint32_t)lane;
+        asm volatile("" : "+v"(l));
+        const uint32_t s = l & 15, rr = l >> 4;
+        const int32_t wbase = (int32_t)(2 * kWin * w) - (int32_t)(2 * z);
+#pragma unroll
+        for (int i = W; i < 32; i += NW) {
+            const uint32_t r = 4 * i + rr, p = r >> 1, q = (p >> 3) & 1;
+            const uint32_t b = (s >> 1) ^ (p & 7), h = (s & 1) ^ q;
+            const uint32_t off = (uint32_t)((int32_t)(r * stride) + wbase + (int32_t)(16 * (2 * b + h)));
+            asm volatile("s_mov_b32 m0, %0\n\t"
+                         "s_nop 0\n\t"
+                         "buffer_load_dwordx4 %1, %2, 0 offen lds"
+                         :: "s"(lbuf + buf * kBuf + i * 1024), "v"(off), "s"(rsrc) : "memory", "m0");
+        }
+    };
+
+    uint32_t S[kLPW][16];
+#pragma unroll
+    for (int L = 0; L < kLPW; ++L)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) S[L][k] = 0;
+
+    const uint32_t p = (uint32_t)lane, q = (p >> 3) & 1;
+    const uint32_t rowa = lbuf + 2 * p * kRowBytes;
+    issue(0, 0);
+    for (uint32_t w = 0; w < nwin; ++w) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();                                   // window w landed; buffer w+1 is free
+        if (w + 1 < nwin) issue(w + 1, (w + 1) & 1);
+        const uint32_t wb = rowa + (w & 1) * kBuf;
+        if (w == 0 && z) {
+            // positions before the row's start (the previous row's bytes, or zeros): clear them in
+            // this lane's two rows (every wave writes the same zeros, each before its own reads)
+            for (uint32_t t = 0; t < z; ++t) {
+                const uint32_t ch = t >> 3, b = ch >> 1, h = ch & 1;
+                const uint32_t o = 16 * (2 * (b ^ (p & 7)) + (h ^ q)) + 2 * (t & 7);
+                asm volatile("ds_write_b16 %0, %1\n\t"
+                             "ds_write_b16 %0, %1 offset:256\n\t"
+                             "s_waitcnt lgkmcnt(0)" :: "v"(wb + o), "v"(0u) : "memory");
+            }
+            // the 16-byte piece holding a row's first symbols straddles its start: a row whose
+            // piece begins before the buffer's range read it as zeros, so reload those symbols
+            const uint32_t zr = z & 7, nfix = (8 - zr) & 7;
+            for (uint32_t h = 0; h < 2 && nfix; ++h) {
+                const uint32_t r = 2 * p + h;
+                if (row0 + r >= a.ncw) break;
+                for (uint32_t t = 0; t < nfix && t < a.n; ++t) {
+                    const uint32_t u = z + t, ch = u >> 3, b = ch >> 1, hh = ch & 1;
+                    const uint32_t o = 16 * (2 * (b ^ (p & 7)) + (hh ^ q)) + 2 * (u & 7) + 256 * h;
+                    const uint32_t v = *reinterpret_cast<const uint16_t *>(tbase + r * a.stride + 2 * t);
+                    asm volatile("ds_write_b16 %0, %1\n\t"
+                                 "s_waitcnt lgkmcnt(0)" :: "v"(wb + o), "v"(v) : "memory");
+                }
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const uint32_t blk = wb + 32 * ((uint32_t)b ^ (p & 7));
+            const uint32_t x0 = blk + 16 * q, x1 = blk + 16 * (q ^ 1);
+            uint4 A0, A1, B0, B1;
+            asm volatile("ds_read_b128 %0, %4\n\t"
+                         "ds_read_b128 %1, %5\n\t"
+                         "ds_read_b128 %2, %4 offset:256\n\t"
+                         "ds_read_b128 %3, %5 offset:256\n\t"
+                         "s_waitcnt lgkmcnt(0)"
+                         : "=&v"(A0), "=&v"(A1), "=&v"(B0), "=&v"(B1)
+                         : "v"(x0), "v"(x1) : "memory");
+            const uint32_t ra[8] = {A0.x, A0.y, A0.z, A0.w, A1.x, A1.y, A1.z, A1.w};
+            const uint32_t rb[8] = {B0.x, B0.y, B0.z, B0.w, B1.x, B1.y, B1.z, B1.w};
+            uint32_t c[16];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                c[2 * t] = __builtin_amdgcn_perm(rb[t], ra[t], 0x05040100u);
+                c[2 * t + 1] = __builtin_amdgcn_perm(rb[t], ra[t], 0x07060302u);
+            }
+            C::template block<kLPW * W>(S[0], c);
+            if constexpr (kLPW * W + 1 < C::NL) C::template block<kLPW * W + 1>(S[1], c);
+        }
+    }
+    // remainders of the lane's two codewords (low halves: row 2p, high halves: row 2p + 1)
+#pragma unroll
+    for (int L = 0; L < kLPW; ++L) {
+        if (kLPW * W + L >= C::NL) break;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const size_t cw = row0 + 2 * p + h;
+            if (cw >= a.ncw) continue;
+            const uint32_t sel = h ? 0x07060302u : 0x05040100u;
+            uint32_t d[8];
+#pragma unroll
+            for (int m = 0; m < 8; ++m) d[m] = __builtin_amdgcn_perm(S[L][2 * m + 1], S[L][2 * m], sel);
+            uint4 *dst = reinterpret_cast<uint4 *>(a.rem + (cw * a.nlp + kLPW * W + L) * 16);
+            dst[0] = make_uint4(d[0], d[1], d[2], d[3]);
+            dst[1] = make_uint4(d[4], d[5], d[6], d[7]);
+        }
+    }
+}
+
+template <class C>
+__global__ void __launch_bounds__(64 * ((C::NL + kLPW - 1) / kLPW)) k_wide_rem(RemArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kBuf];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    constexpr int NW = (C::NL + kLPW - 1) / kLPW;
+    static_assert(NW <= 8, "at most 16 leaders");
+    switch (wave) {
+    case 0: rem_body<C, 0>(a, lds, lane); break;
+    case 1: if constexpr (NW > 1) rem_body<C, 1>(a, lds, lane); break;
+    case 2: if constexpr (NW > 2) rem_body<C, 2>(a, lds, lane); break;
+    case 3: if constexpr (NW > 3) rem_body<C, 3>(a, lds, lane); break;
+    case 4: if constexpr (NW > 4) rem_body<C, 4>(a, lds, lane); break;
+    case 5: if constexpr (NW > 5) rem_body<C, 5>(a, lds, lane); break;
+    case 6: if constexpr (NW > 6) rem_body<C, 6>(a, lds, lane); break;
+    default: if constexpr (NW > 7) rem_body<C, 7>(a, lds, lane); break;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+struct FinishArgs {
+    const uint16_t *rem;
+    uint32_t nlp, ncw, nr, nn;
+    const uint16_t *alpha_to, *index_of;
+    uint8_t leader[kMaxNR];     // syndrome i -> leader slot
+    uint16_t elog[kMaxNR];      // log beta_i = (fcr + i) prim mod NN
+    // encode
+    const uint16_t *qlog;       // [NR][NR] log Q (NN for 0)
+    uint16_t *parity;
+    size_t pstride;             // elements
+    // decode
+    const uint32_t *neras;
+    int32_t *result;
+    uint16_t *syn;              // [ncw][32] polynomial form, flagged codewords only
+    uint32_t *queue;            // [0] count, [1..] flagged codewords
+};
+
+template <bool ENC>
+__global__ void __launch_bounds__(256) k_wide_finish(FinishArgs a) {
+    __shared__ uint16_t sl[8][kMaxNR];
+    const unsigned lane = threadIdx.x & 31, g = threadIdx.x >> 5;
+    const size_t cw = (size_t)blockIdx.x * 8 + g;
+    const bool live = cw < a.ncw;
+    const unsigned NN = a.nn;
+    uint32_t S = 0;
+    if (live && lane < a.nr) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(a.rem + (cw * a.nlp + a.leader[lane]) * 16);
+        const uint4 r0 = src[0], r1 = src[1];
+        const uint32_t rw[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+        const unsigned e = a.elog[lane];
+        unsigned ek = 0;                                   // e * k mod NN
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const unsigned r = (rw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+            if (r) {
+                unsigned x = a.index_of[r] + ek;
+                x = x >= NN ? x - NN : x;
+                S ^= a.alpha_to[x];
+            }
+            ek += e;
+            ek = ek >= NN ? ek - NN : ek;
+        }
+    }
+    if constexpr (ENC) {
+        sl[g][lane] = (uint16_t)(S ? a.index_of[S] : NN);
+        __syncthreads();
+        if (!live || lane >= a.nr) return;
+        const uint16_t *qrow = a.qlog + lane * a.nr;
+        uint32_t par = 0;
+        for (unsigned i = 0; i < a.nr; ++i) {
+            const unsigned s = sl[g][i], qv = qrow[i];
+            if (s != NN && qv != NN) {
+                unsigned x = s + qv;
+                x = x >= NN ? x - NN : x;
+                par ^= a.alpha_to[x];
+            }
+        }
+        a.parity[cw * a.pstride + lane] = (uint16_t)par;
+    } else {
+        const uint64_t nz = __ballot(S != 0);
+        const uint32_t half = (uint32_t)(nz >> (32 * (g & 1)));
+        if (!live || lane != 0) {
+            if (live && half && lane < a.nr) a.syn[cw * kMaxNR + lane] = (uint16_t)S;
+            return;
+        }
+        const bool flagged = half != 0 || (a.neras && a.neras[cw] != 0);
+        if (flagged && lane < a.nr) a.syn[cw * kMaxNR] = (uint16_t)S;
+        if (flagged) {
+            // syndromes of a codeword with erasures but zero syndromes are zero: write them all
+            if (!half)
+                for (unsigned i = 0; i < a.nr; ++i) a.syn[cw * kMaxNR + i] = 0;
+            const uint32_t at = atomicAdd(a.queue, 1u);
+            a.queue[1 + at] = (uint32_t)cw;
+        }
+        a.result[cw] = flagged ? kSentinel : 0;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+struct ErrArgs {
+    DevCodec c;
+    DecodeArgs d;
+    const uint16_t *syn;
+    const uint32_t *queue;
+};
+
+constexpr int kErrWaves = 16;
+constexpr int kErrScratch = 64 + 3 * 32;   // dwords per wave
+
+__device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o, 64);
+    return v;
+}
+
+// x mod nn for x < 2 nn
+__device__ __forceinline__ unsigned red1(unsigned x, unsigned nn) { return x >= nn ? x - nn : x; }
+// x mod nn for any 32-bit x, nn = 2^mm - 1 (Karn's fold, rs_base:648-657): two folds leave x < nn + 2
+__device__ __forceinline__ unsigned fold(unsigned x, unsigned nn, unsigned mm) {
+    x = (x & nn) + (x >> mm);
+    x = (x & nn) + (x >> mm);
+    return red1(x, nn);
+}
+
+__global__ void __launch_bounds__(64 * kErrWaves) k_wide_errors(ErrArgs ea) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+    const DevCodec &c = ea.c;
+    const DecodeArgs &a = ea.d;
+    const unsigned NN = c.nn, A0 = c.nn, NR = c.nroots, FCR = c.fcr, PRM = c.prim, MM = c.mm;
+    const uint32_t nq = ea.queue[0];
+    if ((size_t)blockIdx.x * kErrWaves >= nq) return;      // uniform over the workgroup
+    uint16_t *AT = smem;                                    // alpha_to, NN + 1 entries
+    for (unsigned i = threadIdx.x; i <= NN; i += blockDim.x) AT[i] = c.alpha_to[i];
+    const int wave = threadIdx.x >> 6;
+    const unsigned lane = threadIdx.x & 63;
+    // per-wave scratch: roots (u32 x 64), omega, syndromes, lambda (index form, u16 x 64 each)
+    uint32_t *roots = reinterpret_cast<uint32_t *>(smem + ((NN + 1 + 7) & ~7u)) + wave * kErrScratch;
+    uint16_t *omg = reinterpret_cast<uint16_t *>(roots + 64);
+    uint16_t *slg = omg + 64;
+    uint16_t *llg = slg + 64;
+    __syncthreads();
+    const uint16_t *I = c.index_of;
+    const unsigned len = a.len, pad = c.load - len;
+
+    for (uint32_t qi = blockIdx.x * kErrWaves + wave; qi < nq; qi += gridDim.x * kErrWaves) {
+        const size_t k = ea.queue[1 + qi];
+        uint16_t *data = static_cast<uint16_t *>(a.data) + k * a.data_stride;
+        uint16_t *parity = static_cast<uint16_t *>(a.parity) + k * a.parity_stride;
+        const uint32_t *eras = a.eras ? a.eras + k * a.eras_stride : nullptr;
+        const unsigned no_eras = a.neras ? a.neras[k] : 0;
+        uint32_t *pos = a.positions ? a.positions + k * a.pos_stride : nullptr;
+        uint16_t *corr = a.corr ? static_cast<uint16_t *>(a.corr) + k * a.corr_stride : nullptr;
+        int count;
+        // argument checks of decode_symbols (rs_base:1375-1387)
+        bool bad = no_eras > NR;
+        if (!bad && lane < no_eras) bad = eras[lane] >= len + NR;
+        if (__ballot(bad)) { if (lane == 0) a.result[k] = -1; continue; }
+        const unsigned sp = lane < NR ? ea.syn[k * kMaxNR + lane] : 0u;
+        if (!__ballot(sp != 0)) { if (lane == 0) a.result[k] = 0; continue; }   // 1416-1434
+        const unsigned sl = sp ? I[sp] : A0;                 // syn[lane], index form
+        slg[lane] = (uint16_t)sl;
+
+        // erasure locator (1436-1450): lane j holds lambda[j] (polynomial form)
+        unsigned lam = lane == 0 ? 1u : 0u;
+        if (no_eras > 0) {
+            const unsigned u0 = fold(PRM * (NN - 1 - (eras[0] + pad)), NN, MM);
+            if (lane == 1) lam = AT[u0];
+            for (unsigned i = 1; i < no_eras; ++i) {
+                const unsigned u = fold(PRM * (NN - 1 - (eras[i] + pad)), NN, MM);
+                const unsigned prev = __shfl_up(lam, 1, 64);
+                const unsigned tmp = lane >= 1 && lane <= i + 1 && prev ? I[prev] : A0;
+                if (tmp != A0) lam ^= AT[red1(u + tmp, NN)];
+            }
+        }
+        unsigned b = lam ? I[lam] : A0;                      // b[lane], index form
+        // Berlekamp-Massey (1501-1546); lanes > NR hold lambda = 0, b = A0
+        unsigned r = no_eras, el = no_eras;
+        while (++r <= NR) {
+            const unsigned li = lam ? I[lam] : A0;
+            const unsigned si = lane < r ? slg[r - 1 - lane] : A0;
+            const unsigned term = (li != A0 && si != A0) ? AT[red1(li + si, NN)] : 0u;
+            const unsigned dsum = wave_xor(term);
+            const unsigned discr = dsum ? I[dsum] : A0;
+            const unsigned bprev = __shfl_up(b, 1, 64);
+            const unsigned bsh = lane == 0 ? A0 : bprev;
+            if (discr == A0) {
+                b = lane <= NR ? bsh : A0;
+            } else {
+                const unsigned t = lane == 0 ? lam : lam ^ (bsh != A0 ? AT[red1(discr + bsh, NN)] : 0u);
+                if (2 * el <= r + no_eras - 1) {
+                    el = r + no_eras - el;
+                    b = lane <= NR ? (lam == 0 ? A0 : red1(li + NN - discr, NN)) : A0;
+                } else {
+                    b = lane <= NR ? bsh : A0;
+                }
+                lam = lane <= NR ? t : 0u;
+            }
+        }
+        // lambda to index form, its degree (1549-1553)
+        const unsigned llog = lam ? I[lam] : A0;
+        const uint64_t nzl = __ballot(lam != 0 && lane <= NR);
+        const unsigned deg = 63 - __builtin_clzll(nzl);
+        llg[lane] = (uint16_t)llog;
+        if (deg == 0) {                                      // 1577-1595 (no root can match)
+            if (lane == 0) a.result[k] = -1;
+            continue;
+        }
+        // Chien search (1555-1584): position i = 64 t + lane + 1; reg_j = lambda_j + j i
+        // (NN > 64 kMaxNR for the wide codecs: the per-step increment 64 j needs no reduction)
+        unsigned rg[kMaxNR + 1];
+        uint64_t lmask = 0;
+#pragma unroll
+        for (int j = 1; j <= kMaxNR; ++j) {
+            const unsigned lj = __shfl(llog, j, 64);
+            if (lj != A0 && j <= (int)deg) lmask |= 1ull << j;
+            rg[j] = fold(lj + j * (lane + 1), NN, MM);
+        }
+        count = 0;
+        for (unsigned i0 = 1; i0 <= NN; i0 += 64) {
+            unsigned qv = 1;
+#pragma unroll
+            for (int j0 = 1; j0 <= kMaxNR; j0 += 4) {
+                if (j0 > (int)deg) break;                    // wave-uniform
+#pragma unroll
+                for (int j = j0; j < j0 + 4; ++j)
+                    if (lmask >> j & 1) {                    // wave-uniform
+                        qv ^= AT[rg[j]];
+                        rg[j] = red1(rg[j] + 64u * j, NN);
+                    }
+            }
+            const unsigned i = i0 + lane;
+            const uint64_t hit = __ballot(qv == 0 && i <= NN);
+            if (hit) {
+                const unsigned before = __builtin_popcountll(hit & ((1ull << lane) - 1));
+                if (qv == 0 && i <= NN && count + before < kMaxNR + 1) roots[count + before] = i;
+                count += __builtin_popcountll(hit);
+                if (count >= (int)deg) break;
+            }
+        }
+        if (count != (int)deg || deg == 0) {                // 1577-1595: no corrections
+            if (lane == 0) a.result[k] = -1;
+            continue;
+        }
+        // Omega = S Lambda mod x^NR (1596-1604): lane i <= deg - 1
+        const unsigned deg_omega = deg - 1;
+        if (lane <= deg_omega) {
+            unsigned tmp = 0;
+            for (unsigned j = 0; j <= lane; ++j) {
+                const unsigned sv = slg[lane - j], lv = llg[j];
+                if (sv != A0 && lv != A0) tmp ^= AT[red1(sv + lv, NN)];
+            }
+            omg[lane] = (uint16_t)(tmp ? I[tmp] : A0);
+        }
+        __builtin_amdgcn_wave_barrier();
+        // Forney (1610-1690): lane j handles root j
+        bool fail = false, wrote = false;
+        unsigned cor = 0, loc = 0;
+        if (lane < (unsigned)count) {
+            const unsigned rj = roots[lane];
+            unsigned num1 = 0;
+            for (unsigned i = 0; i <= deg_omega; ++i) {
+                const unsigned ov = omg[i];
+                if (ov != A0) num1 ^= AT[fold(ov + i * rj, NN, MM)];
+            }
+            const unsigned num2 = AT[fold(rj * fold(FCR + NN - 1, NN, MM), NN, MM)];
+            unsigned den = 0;
+            const unsigned top = deg < NR - 1 ? deg : NR - 1;
+            for (int i = (int)(top & ~1u); i >= 0; i -= 2) {
+                const unsigned lv = llg[i + 1];
+                if (lv != A0) den ^= AT[fold(lv + (unsigned)i * rj, NN, MM)];
+            }
+            loc = fold(rj * c.iprim + NN - 1, NN, MM);
+            if (den == 0) fail = true;
+            else if (num1 != 0) {
+                if (loc < pad) fail = true;
+                else {
+                    cor = AT[fold(I[num1] + I[num2] + NN - I[den], NN, MM)];
+                    wrote = true;
+                }
+            }
+        }
+        // the reference walks j = count-1 .. 0 and stops at the first failure: roots above the
+        // highest failing one keep their corrections
+        const uint64_t fm = __ballot(fail);
+        const int jf = fm ? 63 - __builtin_clzll(fm) : -1;
+        if ((int)lane <= jf) wrote = false;
+        if (wrote) {
+            if (loc < NN - NR) data[loc - pad] ^= (uint16_t)cor;
+            else parity[loc - (NN - NR)] ^= (uint16_t)cor;
+            if (corr) corr[lane] = (uint16_t)cor;
+        }
+        count = fm ? -1 : count;
+        if (pos && count > 0 && lane < (unsigned)count) pos[lane] = loc - pad;
+        if (lane == 0) a.result[k] = count;
+    }
+}
+
+} // namespace wide
+
+// ------------------------------------------------------------------------------------------------
+namespace {
+
+template <class C> bool wide_matches(const DevCodec &d) {
+    return d.mm == C::M && d.poly == C::POLY && d.fcr == C::FCR && d.prim == C::PRIM &&
+           d.nroots == C::NR && !d.dual && !d.masked;
+}
+
+template <class C> constexpr uint32_t nlp_of() {
+    return ((C::NL + wide::kLPW - 1) / wide::kLPW) * wide::kLPW;
+}
+
+// Workspace: [queue: 4 + 4 ncw B, rounded to 256] [syn: 64 ncw B] [rem: 32 nlp ncw B]
+struct WideWs {
+    uint32_t *queue;
+    uint16_t *syn;
+    uint16_t *rem;
+};
+
+WideWs carve(void *ws, size_t ncw) {
+    uint8_t *p = static_cast<uint8_t *>(ws);
+    WideWs w;
+    w.queue = reinterpret_cast<uint32_t *>(p);
+    p += ((4 + 4 * ncw) + 255) / 256 * 256;
+    w.syn = reinterpret_cast<uint16_t *>(p);
+    p += 64 * ncw;
+    w.rem = reinterpret_cast<uint16_t *>(p);
+    return w;
+}
+
+template <class C>
+hipError_t launch_rem(const uint8_t *base, size_t stride_bytes, uint32_t n, size_t ncw, uint16_t *rem,
+                      hipStream_t s) {
+    wide::RemArgs r{base, stride_bytes, n, (uint32_t)ncw, rem, nlp_of<C>()};
+    const unsigned grid = (unsigned)((ncw + wide::kRows - 1) / wide::kRows);
+    constexpr int NW = (C::NL + wide::kLPW - 1) / wide::kLPW;
+    hipLaunchKernelGGL((wide::k_wide_rem<C>), dim3(grid), dim3(64 * NW), 0, s, r);
+    return hipGetLastError();
+}
+
+} // namespace
+
+// Per-codec constants of the finishing kernel (syndrome -> leader slot, log beta, log Q).
+struct WideConsts {
+    uint8_t leader[wide::kMaxNR];
+    uint16_t elog[wide::kMaxNR];
+    std::vector<uint16_t> qlog;   // [NR][NR]
+    uint32_t nlp;
+};
+
+int wide_codec_id(const DevCodec &d) {
+    int id = 0, found = -1;
+#define EZRS_WIDE_MATCH(C) \
+    if (found < 0 && wide_matches<wide::WC_##C>(d)) found = id; \
+    ++id;
+    EZRS_WIDE_CODEC_LIST(EZRS_WIDE_MATCH)
+#undef EZRS_WIDE_MATCH
+    return found;
+}
+
+static uint32_t wide_nlp(int id) {
+    int k = 0;
+    uint32_t v = 0;
+#define EZRS_WIDE_NLP(C) if (k++ == id) v = nlp_of<wide::WC_##C>();
+    EZRS_WIDE_CODEC_LIST(EZRS_WIDE_NLP)
+#undef EZRS_WIDE_NLP
+    return v;
+}
+
+size_t wide_ws_bytes(int id, size_t ncw) {
+    return ((4 + 4 * ncw) + 255) / 256 * 256 + 64 * ncw + 32 * (size_t)wide_nlp(id) * ncw;
+}
+
+// Host tables of a wide codec: leader of each syndrome (same coset rule as gen_wide.py) and
+// Q = V^-1 diag(beta^NR) in index form.
+bool wide_build_consts(int id, const CodecMath &m, std::vector<uint16_t> &blob) {
+    const unsigned NN = m.nn, NR = m.spec.nroots;
+    if (NR > wide::kMaxNR) return false;
+    const Field &gf = m.gf;
+    // leaders in order of first appearance
+    std::vector<unsigned> lead;
+    std::vector<uint8_t> li(NR);
+    std::vector<uint16_t> el(NR);
+    for (unsigned i = 0; i < NR; ++i) {
+        const unsigned e = (unsigned)(((uint64_t)(m.spec.fcr + i) * m.spec.prim) % NN);
+        el[i] = (uint16_t)e;
+        unsigned mn = e, x = e;
+        do { x = (unsigned)((2ull * x) % NN); if (x < mn) mn = x; } while (x != e);
+        unsigned slot = 0;
+        while (slot < lead.size() && lead[slot] != mn) ++slot;
+        if (slot == lead.size()) lead.push_back(mn);
+        li[i] = (uint8_t)slot;
+    }
+    // V[i][k] = beta_i^(NR-1-k); invert by Gauss-Jordan
+    std::vector<unsigned> V(NR * NR), Inv(NR * NR, 0);
+    for (unsigned i = 0; i < NR; ++i) {
+        for (unsigned k = 0; k < NR; ++k)
+            V[i * NR + k] = gf.pow_alpha((unsigned)(((uint64_t)el[i] * (NR - 1 - k)) % NN));
+        Inv[i * NR + i] = 1;
+    }
+    auto inv = [&](unsigned a) { return gf.alpha_to[(NN - gf.index_of[a]) % NN]; };
+    for (unsigned col = 0; col < NR; ++col) {
+        unsigned piv = col;
+        while (piv < NR && !V[piv * NR + col]) ++piv;
+        if (piv == NR) return false;
+        if (piv != col)
+            for (unsigned k = 0; k < NR; ++k) {
+                std::swap(V[piv * NR + k], V[col * NR + k]);
+                std::swap(Inv[piv * NR + k], Inv[col * NR + k]);
+            }
+        const unsigned f = inv(V[col * NR + col]);
+        for (unsigned k = 0; k < NR; ++k) {
+            V[col * NR + k] = gf.mul(V[col * NR + k], f);
+            Inv[col * NR + k] = gf.mul(Inv[col * NR + k], f);
+        }
+        for (unsigned r = 0; r < NR; ++r) {
+            if (r == col || !V[r * NR + col]) continue;
+            const unsigned g = V[r * NR + col];
+            for (unsigned k = 0; k < NR; ++k) {
+                V[r * NR + k] ^= gf.mul(g, V[col * NR + k]);
+                Inv[r * NR + k] ^= gf.mul(g, Inv[col * NR + k]);
+            }
+        }
+    }
+    // blob: leader[32] (as u16) | elog[32] | qlog[NR*NR]
+    blob.assign(2 * wide::kMaxNR + NR * NR, 0);
+    for (unsigned i = 0; i < NR; ++i) {
+        blob[i] = li[i];
+        blob[wide::kMaxNR + i] = el[i];
+    }
+    for (unsigned k = 0; k < NR; ++k)
+        for (unsigned i = 0; i < NR; ++i) {
+            const unsigned bn = gf.pow_alpha((unsigned)(((uint64_t)el[i] * NR) % NN));
+            const unsigned q = gf.mul(Inv[k * NR + i], bn);
+            blob[2 * wide::kMaxNR + k * NR + i] = (uint16_t)(q ? gf.index_of[q] : NN);
+        }
+    (void)id;
+    return true;
+}
+
+static wide::FinishArgs finish_args(const DevCodec &d, int id, const uint16_t *blob_host,
+                                    const uint16_t *qlog_dev, size_t ncw, uint16_t *rem) {
+    wide::FinishArgs f{};
+    f.rem = rem;
+    f.nlp = wide_nlp(id);
+    f.ncw = (uint32_t)ncw;
+    f.nr = d.nroots;
+    f.nn = d.nn;
+    f.alpha_to = d.alpha_to;
+    f.index_of = d.index_of;
+    for (unsigned i = 0; i < d.nroots; ++i) {
+        f.leader[i] = (uint8_t)blob_host[i];
+        f.elog[i] = blob_host[wide::kMaxNR + i];
+    }
+    f.qlog = qlog_dev;
+    return f;
+}
+
+bool wide_can_encode(const DevCodec &, const EncodeArgs &a) {
+    return a.ncw <= 0xFFFFFFFFu && (a.ncw <= 1 || 2 * a.data_stride * (wide::kRows - 1) < 0x80000000u);
+}
+
+bool wide_can_decode(const DevCodec &d, const DecodeArgs &a) {
+    const bool inline_par = a.parity == static_cast<uint16_t *>(a.data) + a.len &&
+                            a.parity_stride == a.data_stride;
+    return inline_par && a.ncw <= 0xFFFFFFFFu &&
+           (a.ncw <= 1 || 2 * a.data_stride * (wide::kRows - 1) < 0x80000000u) &&
+           (a.ncw <= 1 || a.data_stride >= (size_t)a.len + d.nroots);
+}
+
+hipError_t launch_wide_encode(int id, const DevCodec &d, const EncodeArgs &a, const uint16_t *blob_host,
+                              const uint16_t *qlog_dev, void *ws, hipStream_t s) {
+    if (a.ncw == 0) return hipSuccess;
+    WideWs w = carve(ws, a.ncw);
+    const size_t sb = 2 * (a.ncw > 1 ? a.data_stride : (size_t)a.len);
+    int k = 0;
+    hipError_t e = hipSuccess;
+#define EZRS_WIDE_ENC(C) \
+    if (k++ == id) e = launch_rem<wide::WC_##C>(static_cast<const uint8_t *>(a.data), sb, a.len, a.ncw, w.rem, s);
+    EZRS_WIDE_CODEC_LIST(EZRS_WIDE_ENC)
+#undef EZRS_WIDE_ENC
+    if (e != hipSuccess) return e;
+    wide::FinishArgs f = finish_args(d, id, blob_host, qlog_dev, a.ncw, w.rem);
+    f.parity = static_cast<uint16_t *>(a.parity);
+    f.pstride = a.parity_stride;
+    hipLaunchKernelGGL(wide::k_wide_finish<true>, dim3((unsigned)((a.ncw + 7) / 8)), dim3(256), 0, s, f);
+    return hipGetLastError();
+}
+
+hipError_t launch_wide_decode(int id, const DevCodec &d, const DecodeArgs &a, const uint16_t *blob_host,
+                              const uint16_t *qlog_dev, void *ws, hipStream_t s) {
+    if (a.ncw == 0) return hipSuccess;
+    WideWs w = carve(ws, a.ncw);
+    hipError_t e = hipMemsetAsync(w.queue, 0, 4, s);
+    if (e != hipSuccess) return e;
+    const size_t sb = 2 * (a.ncw > 1 ? a.data_stride : (size_t)a.len + d.nroots);
+    int k = 0;
+#define EZRS_WIDE_DEC(C) \
+    if (k++ == id) e = launch_rem<wide::WC_##C>(static_cast<const uint8_t *>(a.data), sb, a.len + d.nroots, a.ncw, w.rem, s);
+    EZRS_WIDE_CODEC_LIST(EZRS_WIDE_DEC)
+#undef EZRS_WIDE_DEC
+    if (e != hipSuccess) return e;
+    wide::FinishArgs f = finish_args(d, id, blob_host, qlog_dev, a.ncw, w.rem);
+    f.neras = a.neras;
+    f.result = a.result;
+    f.syn = w.syn;
+    f.queue = w.queue;
+    hipLaunchKernelGGL(wide::k_wide_finish<false>, dim3((unsigned)((a.ncw + 7) / 8)), dim3(256), 0, s, f);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    wide::ErrArgs ea{d, a, w.syn, w.queue};
+    const size_t smem = (((size_t)d.nn + 1 + 7) & ~(size_t)7) * 2 + wide::kErrWaves * wide::kErrScratch * 4;
+    const unsigned grid = (unsigned)(d.ncu > 0 ? d.ncu : 256);
+    static const hipError_t attr = hipFuncSetAttribute(
+        reinterpret_cast<const void *>(&wide::k_wide_errors),
+        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (attr != hipSuccess) return attr;
+    hipLaunchKernelGGL(wide::k_wide_errors, dim3(grid), dim3(64 * wide::kErrWaves), smem, s, ea);
+    return hipGetLastError();
+}
+
+} // namespace ezrs
