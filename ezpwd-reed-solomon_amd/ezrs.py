@@ -78,6 +78,11 @@ def lib():
         L.ezrs_encode_rows_host.argtypes = [_vp, _vp, _sz, _u, _sz, _sz]
         L.ezrs_decode_host.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _vp, _sz, _vp, _vp, _vp,
                                        _sz, _vp, _sz, _sz, _sz]
+        L.ezrs_stream_encoded_bound.argtypes = [_vp, _sz, _u]
+        L.ezrs_stream_encoded_bound.restype = _sz
+        L.ezrs_stream_encode.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, C.POINTER(_sz)]
+        L.ezrs_stream_decode.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, C.POINTER(_sz),
+                                         C.POINTER(_sz)]
         L.ezrs_host_alloc.argtypes = [C.POINTER(_vp), _sz]
         L.ezrs_host_free.argtypes = [_vp]
         L.ezbch_last_error.restype = C.c_char_p
@@ -280,6 +285,33 @@ class Codec:
             self._h, _np(data), ds, length, _np(parity), ps, _np(eras), es, _np(neras),
             _np(result), _np(positions), qs, _np(corr), cs, ncw, chunk), "ezrs_decode_host")
         return result
+
+
+    # -- rsencode wire format -------------------------------------------------------------------
+    def stream_encode(self, data, chunk=128):
+        """bytes -> rsencode-format bytes (each chunk followed by its parity; include/ezrs.h
+        ezrs_stream_encode).  Returns (encoded, ok); ok is False when a trailing partial symbol
+        stopped the stream (the whole chunks before it are encoded, as rsencode does)."""
+        src = np.frombuffer(bytes(data), np.uint8)
+        cap = int(lib().ezrs_stream_encoded_bound(self._h, src.size, chunk)) or 1
+        out = np.zeros(cap, np.uint8)
+        n = _sz(0)
+        rc = lib().ezrs_stream_encode(self._h, _np(src) if src.size else None, src.size, chunk,
+                                      _np(out), cap, C.byref(n))
+        if rc not in (0, -errno.EMSGSIZE):
+            _check(rc, "ezrs_stream_encode")
+        return out[:n.value].tobytes(), rc == 0
+
+    def stream_decode(self, data, chunk=128):
+        """rsencode-format bytes -> (decoded bytes, chunks that failed to decode, ok)."""
+        src = np.frombuffer(bytes(data), np.uint8)
+        out = np.zeros(max(src.size, 1), np.uint8)
+        n, nf = _sz(0), _sz(0)
+        rc = lib().ezrs_stream_decode(self._h, _np(src) if src.size else None, src.size, chunk,
+                                      _np(out), out.size, C.byref(n), C.byref(nf))
+        if rc not in (0, -errno.EMSGSIZE):
+            _check(rc, "ezrs_stream_decode")
+        return out[:n.value].tobytes(), nf.value, rc == 0
 
 
 class BCH:

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define EZRS_ABI_VERSION 3
+#define EZRS_ABI_VERSION 4
 
 typedef struct ezrs_codec ezrs_codec;
 
@@ -148,6 +148,25 @@ int ezrs_decode_host(ezrs_codec *codec, void *data, size_t data_stride, unsigned
                      size_t eras_stride, const uint32_t *neras, int32_t *result,
                      uint32_t *positions, size_t pos_stride, void *corr, size_t corr_stride,
                      size_t ncw, size_t chunk);
+
+/* rsencode wire format (replaces the per-chunk loop of rsencode.C:93-163, whose encode/decode
+ * helpers call RS_t::encode / RS_t::decode once per chunk).  The input is cut into chunks of
+ * `chunk` data symbols (the last may be shorter); each chunk is written followed by its NROOTS
+ * parity symbols; symbols wider than 8 bits are big-endian on the wire (rsencode.C:52-85).  All
+ * chunks of a call are one batch on the device.
+ *  - ezrs_stream_encode: out receives at most ezrs_stream_encoded_bound(in_bytes) bytes.
+ *  - ezrs_stream_decode: out receives the corrected data without parity (<= in_bytes bytes); a
+ *    chunk the decoder cannot correct is passed on as the decoder left it, as rsencode does, and
+ *    counted in *n_failed (nullable).
+ * A trailing piece that cannot form a chunk (an odd byte for 16-bit symbols; for decode, fewer
+ * than NROOTS + 1 symbols -- rsencode.C:110-111, 140-141) returns -EMSGSIZE after the whole
+ * chunks before it were written (*out_bytes counts them).  -EINVAL: chunk 0 or above the codec's
+ * load; -ENOSPC: out_cap too small. */
+size_t ezrs_stream_encoded_bound(const ezrs_codec *codec, size_t in_bytes, unsigned chunk);
+int ezrs_stream_encode(ezrs_codec *codec, const void *in, size_t in_bytes, unsigned chunk,
+                       void *out, size_t out_cap, size_t *out_bytes);
+int ezrs_stream_decode(ezrs_codec *codec, const void *in, size_t in_bytes, unsigned chunk,
+                       void *out, size_t out_cap, size_t *out_bytes, size_t *n_failed);
 
 /* Pinned host memory for the host-memory forms (hipHostMalloc / hipHostFree). */
 int ezrs_host_alloc(void **ptr, size_t bytes);
