@@ -213,12 +213,15 @@ def cpu_baselines(seconds=4.0):
             "physical_cores": info["physical_cores"], "rows": rows}
 
 
-def load_traffic(kernel_call):
-    """HBM bytes per launch from the committed PMC summary (profiles/traffic.json), if any."""
+def load_traffic(workload, kernel_call, ncw):
+    """HBM bytes per launch of `kernel_call` in `workload` from the committed PMC summary
+    (profiles/traffic.json, tools/traffic_json.py), when it was measured at this batch size."""
     fn = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(fn) as f:
-            t = json.load(f)
+            t = json.load(f).get(workload, {})
+        if t.get("codewords") != ncw:
+            return None
         return t.get(kernel_call, {}).get("hbm_bytes_per_launch")
     except Exception:
         return None
@@ -317,7 +320,7 @@ def bench_rs_errors(args):
                        "parallelism": f"shard{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None, "kernel": dom,
+                         "traffic": load_traffic(args.workload, dom, ncw), "kernel": dom,
                          "avg_ms": {"ezrs_encode": round(enc_ms, 4), "ezrs_decode": round(dec_ms, 4)}},
             "cpu_baseline": None}), flush=True)
     if world > 1:
@@ -402,7 +405,7 @@ def bench_c5(args):
                        "parallelism": f"shard{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": load_traffic(dom), "kernel": dom,
+                         "traffic": load_traffic("c5", dom, ncw), "kernel": dom,
                          "avg_ms": {"ezbch_encode": round(enc_ms, 4),
                                     "ezbch_decode": round(dec_ms, 4)}},
             "cpu_baseline": None}), flush=True)
@@ -635,7 +638,7 @@ def main():
     achieved = ncw * per_cw / (ms * 1e-3) / 1e9
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": load_traffic(dom), "kernel": dom,
+                "traffic": load_traffic(args.workload, dom, ncw), "kernel": dom,
                 "algorithmic_bytes_per_launch": ncw * per_cw,
                 "avg_ms": {"ezrs_encode": round(enc_ms, 4), "ezrs_decode": round(dec_ms, 4)}}
 

@@ -283,6 +283,8 @@ struct ErrArgs {
 
 constexpr int kErrWaves = 16;
 constexpr int kErrScratch = 64 + 3 * 32;   // dwords per wave
+constexpr unsigned kExt = 8192;            // antilog entries past NN (lazy reduction)
+constexpr unsigned kSeg = 1025;            // Chien positions per lane (64 kSeg >= 65535, odd)
 
 __device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
 #pragma unroll
@@ -306,12 +308,12 @@ __global__ void __launch_bounds__(64 * kErrWaves) k_wide_errors(ErrArgs ea) {
     const unsigned NN = c.nn, A0 = c.nn, NR = c.nroots, FCR = c.fcr, PRM = c.prim, MM = c.mm;
     const uint32_t nq = ea.queue[0];
     if ((size_t)blockIdx.x * kErrWaves >= nq) return;      // uniform over the workgroup
-    uint16_t *AT = smem;                                    // alpha_to, NN + 1 entries
-    for (unsigned i = threadIdx.x; i <= NN; i += blockDim.x) AT[i] = c.alpha_to[i];
+    uint16_t *AT = smem;                          // alpha^(e mod NN) for e < NN + kExt (Chien)
+    for (unsigned i = threadIdx.x; i < NN + kExt; i += blockDim.x) AT[i] = c.alpha_to[i < NN ? i : i - NN];
     const int wave = threadIdx.x >> 6;
     const unsigned lane = threadIdx.x & 63;
     // per-wave scratch: roots (u32 x 64), omega, syndromes, lambda (index form, u16 x 64 each)
-    uint32_t *roots = reinterpret_cast<uint32_t *>(smem + ((NN + 1 + 7) & ~7u)) + wave * kErrScratch;
+    uint32_t *roots = reinterpret_cast<uint32_t *>(smem + ((NN + kExt + 7) & ~7u)) + wave * kErrScratch;
     uint16_t *omg = reinterpret_cast<uint16_t *>(roots + 64);
     uint16_t *slg = omg + 64;
     uint16_t *llg = slg + 64;
@@ -382,30 +384,38 @@ __global__ void __launch_bounds__(64 * kErrWaves) k_wide_errors(ErrArgs ea) {
             if (lane == 0) a.result[k] = -1;
             continue;
         }
-        // Chien search (1555-1584): position i = 64 t + lane + 1; reg_j = lambda_j + j i
-        // (NN > 64 kMaxNR for the wide codecs: the per-step increment 64 j needs no reduction)
-        unsigned rg[kMaxNR + 1];
-        uint64_t lmask = 0;
+        // Chien search (1555-1584): lane l walks positions i = 1 + l S + t, t = 0..S-1 (S = kSeg,
+        // odd): reg_j = lambda_j + j i.  Lanes 1025 positions apart spread every term's table reads
+        // over the LDS banks (j i mod 2^16 - 1 rotates the position bits); the table is extended
+        // by kExt entries, so reg_j is reduced only every 256 steps, and a zero coefficient is a
+        // mask, not a branch.  Roots are collected unordered and sorted below (the reference's
+        // ascending-i order).
+        const unsigned seg = kSeg;
+        const unsigned i_l = 1 + lane * seg;
+        unsigned rg[kMaxNR + 1], msk[kMaxNR + 1];
 #pragma unroll
         for (int j = 1; j <= kMaxNR; ++j) {
             const unsigned lj = __shfl(llog, j, 64);
-            if (lj != A0 && j <= (int)deg) lmask |= 1ull << j;
-            rg[j] = fold(lj + j * (lane + 1), NN, MM);
+            msk[j] = (lj != A0 && j <= (int)deg) ? 0xFFFFFFFFu : 0u;   // wave-uniform
+            rg[j] = fold(lj + j * i_l, NN, MM);
         }
         count = 0;
-        for (unsigned i0 = 1; i0 <= NN; i0 += 64) {
+        for (unsigned t = 0; t < seg; ++t) {
             unsigned qv = 1;
 #pragma unroll
             for (int j0 = 1; j0 <= kMaxNR; j0 += 4) {
                 if (j0 > (int)deg) break;                    // wave-uniform
 #pragma unroll
-                for (int j = j0; j < j0 + 4; ++j)
-                    if (lmask >> j & 1) {                    // wave-uniform
-                        qv ^= AT[rg[j]];
-                        rg[j] = red1(rg[j] + 64u * j, NN);
-                    }
+                for (int j = j0; j < j0 + 4; ++j) {
+                    qv ^= AT[rg[j]] & msk[j];
+                    rg[j] += j;
+                }
             }
-            const unsigned i = i0 + lane;
+            if ((t & 255) == 255) {
+#pragma unroll
+                for (int j = 1; j <= kMaxNR; ++j) rg[j] = red1(rg[j], NN);
+            }
+            const unsigned i = i_l + t;
             const uint64_t hit = __ballot(qv == 0 && i <= NN);
             if (hit) {
                 const unsigned before = __builtin_popcountll(hit & ((1ull << lane) - 1));
@@ -413,6 +423,17 @@ __global__ void __launch_bounds__(64 * kErrWaves) k_wide_errors(ErrArgs ea) {
                 count += __builtin_popcountll(hit);
                 if (count >= (int)deg) break;
             }
+        }
+        if (count == (int)deg) {                             // ascending order (rank sort)
+            __builtin_amdgcn_wave_barrier();
+            unsigned v = 0, rank = 0;
+            if (lane < (unsigned)count) {
+                v = roots[lane];
+                for (int s2 = 0; s2 < count; ++s2) rank += roots[s2] < v;
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (lane < (unsigned)count) roots[rank] = v;
+            __builtin_amdgcn_wave_barrier();
         }
         if (count != (int)deg || deg == 0) {                // 1577-1595: no corrections
             if (lane == 0) a.result[k] = -1;
@@ -684,7 +705,7 @@ hipError_t launch_wide_decode(int id, const DevCodec &d, const DecodeArgs &a, co
     hipLaunchKernelGGL(wide::k_wide_finish<false>, dim3((unsigned)((a.ncw + 7) / 8)), dim3(256), 0, s, f);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     wide::ErrArgs ea{d, a, w.syn, w.queue};
-    const size_t smem = (((size_t)d.nn + 1 + 7) & ~(size_t)7) * 2 + wide::kErrWaves * wide::kErrScratch * 4;
+    const size_t smem = (((size_t)d.nn + wide::kExt + 7) & ~(size_t)7) * 2 + wide::kErrWaves * wide::kErrScratch * 4;
     const unsigned grid = (unsigned)(d.ncu > 0 ? d.ncu : 256);
     static const hipError_t attr = hipFuncSetAttribute(
         reinterpret_cast<const void *>(&wide::k_wide_errors),
