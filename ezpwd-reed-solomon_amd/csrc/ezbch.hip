@@ -10,15 +10,16 @@
 //            8*len), reported in ascending order (the reference's order is unpinned).
 //
 // Kernels: one lane per codeword, 256-codeword workgroups.
-//   k_bch_encode    byte-at-a-time LFSR over the data with a left-justified 64-bit remainder and a
-//                   256-entry step table in LDS; each row is read as aligned dwords (v_alignbyte).
+//   k_bch_encode    byte-at-a-time LFSR over the data with a left-justified remainder of NW 64-bit
+//                   words (NW = 1, 2, 4: ecc_bits <= 64, 128, 256) and a 256-entry step table in LDS;
+//                   each row is read as aligned dwords (v_alignbyte).
 //   k_bch_decode<T> the same remainder XOR the received ECC; zero -> result 0.  Otherwise, in the
 //                   same lane: syndromes S_1..S_2t from the set bits of the difference, binary
 //                   Berlekamp-Massey (odd steps; static register arrays), and the locator's roots:
 //                   degree 1 directly, degrees 2..4 as an affine GF(2)-linear equation
 //                   A4 y^4 + A2 y^2 + A1 y = delta solved by elimination over the m basis bits,
 //                   degree > 4 by a Chien search over the codeword's bit positions.
-// Device limits: t <= 8 and m*t <= 64 (the ECC fits one 64-bit register); other init_bch-valid
+// Device limits: t <= 16 and ecc_bits <= 256 (four 64-bit remainder words); other init_bch-valid
 // codecs are refused with -ENOTSUP at creation.  There is no CPU path.
 #include <hip/hip_runtime.h>
 
@@ -35,7 +36,8 @@
 
 namespace {
 
-constexpr int kMaxT = 8;
+constexpr int kMaxT = 16;
+constexpr int kMaxNW = 4;                    // 64-bit words of the widest remainder
 constexpr int kMaxM = 15;
 constexpr int kThreads = 256;
 constexpr int kEBADMSG = 74, kEINVAL = 22;   // Linux errno values, negated as decode_bch returns them
@@ -43,8 +45,9 @@ constexpr int kEBADMSG = 74, kEINVAL = 22;   // Linux errno values, negated as d
 struct DevBch {
     int m, n, t, ecc_bits, ecc_bytes;
     int lds_tabs;             // exp/log tables staged in LDS (m <= 12)
-    uint64_t emask;           // the ecc_bits significant bits of a left-justified remainder
-    const uint64_t *step;     // [256] byte-step remainder table
+    int nw;                   // 64-bit words of the remainder (1, 2, 4)
+    uint64_t emask[kMaxNW];   // the ecc_bits significant bits of a left-justified remainder
+    const uint64_t *step;     // [256][nw] byte-step remainder table
     const uint16_t *ex;       // [2n] alpha^i
     const uint16_t *lg;       // [n+1] log_alpha (lg[0] unused)
 };
@@ -65,9 +68,10 @@ struct BchArgs {
 
 constexpr size_t kLdsLimit = 65536;
 
-// LDS layout: [0, 2048) byte-step table | exp/log tables (decode, m <= 12) | staged rows
+// LDS layout: [0, 2048 nw) byte-step table | exp/log tables (decode, m <= 12) | staged rows
+__host__ __device__ inline size_t tabs_offset(const DevBch &b) { return (size_t)2048 * b.nw; }
 __host__ __device__ inline size_t rows_offset(const DevBch &b, bool tabs) {
-    return 2048 + (tabs && b.lds_tabs ? (((size_t)3 * b.n + 1) * 2 + 15) / 16 * 16 : 0);
+    return tabs_offset(b) + (tabs && b.lds_tabs ? (((size_t)3 * b.n + 1) * 2 + 15) / 16 * 16 : 0);
 }
 
 size_t lds_bytes(const DevBch &b, bool tabs, const BchArgs &a) {
@@ -119,18 +123,31 @@ __device__ __forceinline__ void for_each_byte(const uint8_t *p, unsigned len, F 
     }
 }
 
-__device__ __forceinline__ uint64_t data_remainder(const uint64_t *step, const uint8_t *p,
-                                                   unsigned len) {
-    uint64_t r = 0;
-    for_each_byte(p, len, [&](uint32_t byte) { r = (r << 8) ^ step[(uint32_t)(r >> 56) ^ byte]; });
+// A left-justified multiword remainder: w[0] holds the most significant 64 bits.
+template <int NW> struct Rem {
+    uint64_t w[NW];
+};
+
+template <int NW>
+__device__ __forceinline__ Rem<NW> data_remainder(const uint64_t *step, const uint8_t *p,
+                                                  unsigned len) {
+    Rem<NW> r;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) r.w[i] = 0;
+    for_each_byte(p, len, [&](uint32_t byte) {
+        const uint64_t *s = step + NW * ((uint32_t)(r.w[0] >> 56) ^ byte);
+#pragma unroll
+        for (int i = 0; i < NW; ++i)
+            r.w[i] = ((r.w[i] << 8) | (i + 1 < NW ? r.w[i + 1 < NW ? i + 1 : i] >> 56 : 0)) ^ s[i];
+    });
     return r;
 }
 
 __device__ __forceinline__ void stage_tables(const DevBch &b, uint8_t *smem, bool tabs) {
     uint64_t *step = reinterpret_cast<uint64_t *>(smem);
-    for (int i = threadIdx.x; i < 256; i += kThreads) step[i] = b.step[i];
+    for (int i = threadIdx.x; i < 256 * b.nw; i += kThreads) step[i] = b.step[i];
     if (tabs && b.lds_tabs) {
-        uint16_t *ex = reinterpret_cast<uint16_t *>(smem + 2048), *lg = ex + 2 * b.n;
+        uint16_t *ex = reinterpret_cast<uint16_t *>(smem + tabs_offset(b)), *lg = ex + 2 * b.n;
         for (int i = threadIdx.x; i < 2 * b.n; i += kThreads) ex[i] = b.ex[i];
         for (int i = threadIdx.x; i <= b.n; i += kThreads) lg[i] = b.lg[i];
     }
@@ -157,15 +174,16 @@ __device__ __forceinline__ const uint8_t *block_rows(uint8_t *smem, const DevBch
     return rows + off + threadIdx.x * a.dstride;
 }
 
+template <int NW>
 __global__ void __launch_bounds__(kThreads) k_bch_encode(DevBch b, BchArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     stage_tables(b, smem, false);
     const uint8_t *row = block_rows(smem, b, false, a);
     const size_t k = (size_t)blockIdx.x * kThreads + threadIdx.x;
     if (k >= a.ncw) return;
-    const uint64_t r = data_remainder(reinterpret_cast<const uint64_t *>(smem), row, a.len);
+    const Rem<NW> r = data_remainder<NW>(reinterpret_cast<const uint64_t *>(smem), row, a.len);
     uint8_t *e = a.ecc + k * a.estride;
-    for (int i = 0; i < b.ecc_bytes; ++i) e[i] = (uint8_t)(r >> (56 - 8 * i));
+    for (int i = 0; i < b.ecc_bytes; ++i) e[i] = (uint8_t)(r.w[i >> 3] >> (56 - 8 * (i & 7)));
 }
 
 // y -> A4 y^4 + A2 y^2 + A1 y is GF(2)-linear.  With the images of the polynomial-basis vectors
@@ -292,26 +310,33 @@ __device__ __forceinline__ uint32_t coef(const uint32_t (&C)[W]) {
 
 // decode_bch on the masked ECC difference r (left-justified): the count and the ascending error
 // locations, or -EBADMSG.
-template <int T>
-__device__ int locate(const DevBch &b, const GF &f, uint64_t r, uint32_t nbits,
+template <int T, int NW>
+__device__ int locate(const DevBch &b, const GF &f, Rem<NW> r, uint32_t nbits,
                       uint32_t (&loc)[T]) {
-    if (!r) return 0;                       // only unused ECC bits differ
+    uint64_t any = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) any |= r.w[i];
+    if (!any) return 0;                     // only unused ECC bits differ
     const uint32_t n = (uint32_t)b.n;
     uint32_t S[2 * T + 1];
 #pragma unroll
     for (int j = 0; j <= 2 * T; ++j) S[j] = 0;
-    while (r) {                             // S_j = r(alpha^j), j odd
-        const int lz = __clzll(r);
-        r &= ~(0x8000000000000000ull >> lz);
-        const uint32_t p = (uint32_t)(b.ecc_bits - 1 - lz);
-        uint32_t p2 = 2 * p;
-        if (p2 >= n) p2 -= n;
-        uint32_t e = p;
 #pragma unroll
-        for (int j = 1; j < 2 * T; j += 2) {
-            S[j] ^= f.ex[e];
-            e += p2;
-            if (e >= n) e -= n;
+    for (int wi = 0; wi < NW; ++wi) {
+        uint64_t x = r.w[wi];
+        while (x) {                         // S_j = r(alpha^j), j odd
+            const int lz = __clzll(x);
+            x &= ~(0x8000000000000000ull >> lz);
+            const uint32_t p = (uint32_t)(b.ecc_bits - 1 - (64 * wi + lz));
+            uint32_t p2 = 2 * p;
+            if (p2 >= n) p2 -= n;
+            uint32_t e = p;
+#pragma unroll
+            for (int j = 1; j < 2 * T; j += 2) {
+                S[j] ^= f.ex[e];
+                e += p2;
+                if (e >= n) e -= n;
+            }
         }
     }
 #pragma unroll
@@ -404,7 +429,7 @@ __device__ int locate(const DevBch &b, const GF &f, uint64_t r, uint32_t nbits,
     return L;
 }
 
-template <int T>
+template <int T, int NW>
 __global__ void __launch_bounds__(kThreads) k_bch_decode(DevBch b, BchArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     stage_tables(b, smem, true);
@@ -416,16 +441,21 @@ __global__ void __launch_bounds__(kThreads) k_bch_decode(DevBch b, BchArgs a) {
         return;
     }
     uint8_t *d = a.wdata + k * a.dstride, *e = a.ecc + k * a.estride;
-    uint64_t r = data_remainder(reinterpret_cast<const uint64_t *>(smem), row, a.len);
-    for (int i = 0; i < b.ecc_bytes; ++i) r ^= (uint64_t)e[i] << (56 - 8 * i);
-    if (!r) {
+    Rem<NW> r = data_remainder<NW>(reinterpret_cast<const uint64_t *>(smem), row, a.len);
+    for (int i = 0; i < b.ecc_bytes; ++i) r.w[i >> 3] ^= (uint64_t)e[i] << (56 - 8 * (i & 7));
+    uint64_t any = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) any |= r.w[i];
+    if (!any) {
         a.result[k] = 0;
         return;
     }
-    const uint16_t *sx = reinterpret_cast<const uint16_t *>(smem + 2048);
+#pragma unroll
+    for (int i = 0; i < NW; ++i) r.w[i] &= b.emask[i];
+    const uint16_t *sx = reinterpret_cast<const uint16_t *>(smem + tabs_offset(b));
     const GF f{b.lds_tabs ? sx : b.ex, b.lds_tabs ? sx + 2 * b.n : b.lg, b.n};
     uint32_t loc[T];
-    const int cnt = locate<T>(b, f, r & b.emask, 8u * a.len + (uint32_t)b.ecc_bits, loc);
+    const int cnt = locate<T, NW>(b, f, r, 8u * a.len + (uint32_t)b.ecc_bits, loc);
     a.result[k] = cnt;
 #pragma unroll
     for (int i = 0; i < T; ++i) {
@@ -441,7 +471,10 @@ __global__ void __launch_bounds__(kThreads) k_bch_decode(DevBch b, BchArgs a) {
 hipError_t launch_encode(const DevBch &b, BchArgs a, hipStream_t s) {
     const unsigned grid = (unsigned)((a.ncw + kThreads - 1) / kThreads);
     a.staged = want_staging(b, false, a);
-    hipLaunchKernelGGL(k_bch_encode, dim3(grid), dim3(kThreads), lds_bytes(b, false, a), s, b, a);
+    const size_t sh = lds_bytes(b, false, a);
+    if (b.nw == 1) hipLaunchKernelGGL(k_bch_encode<1>, dim3(grid), dim3(kThreads), sh, s, b, a);
+    else if (b.nw == 2) hipLaunchKernelGGL(k_bch_encode<2>, dim3(grid), dim3(kThreads), sh, s, b, a);
+    else hipLaunchKernelGGL(k_bch_encode<4>, dim3(grid), dim3(kThreads), sh, s, b, a);
     return hipGetLastError();
 }
 
@@ -449,18 +482,23 @@ hipError_t launch_decode(const DevBch &b, BchArgs a, hipStream_t s) {
     const unsigned grid = (unsigned)((a.ncw + kThreads - 1) / kThreads);
     a.staged = want_staging(b, true, a);
     const size_t sh = lds_bytes(b, true, a);
-    switch (b.t) {
-#define EZBCH_CASE(T)                                                                         \
-    case T:                                                                                   \
-        hipLaunchKernelGGL(k_bch_decode<T>, dim3(grid), dim3(kThreads), sh, s, b, a);         \
-        break;
-        EZBCH_CASE(1) EZBCH_CASE(2) EZBCH_CASE(3) EZBCH_CASE(4)
-        EZBCH_CASE(5) EZBCH_CASE(6) EZBCH_CASE(7) EZBCH_CASE(8)
-#undef EZBCH_CASE
-    default:
-        return hipErrorInvalidValue;
+    // (T, NW) instantiations: NW = 1 for ecc_bits <= 64 (t <= 12 since m >= 5), NW = 2 for
+    // ecc_bits <= 128 (m t > 64: t >= 5), NW = 4 for ecc_bits <= 256 (t >= 9)
+#define EZBCH_CASE(T, NW)                                                                     \
+    if (b.t == T && b.nw == NW) {                                                             \
+        hipLaunchKernelGGL((k_bch_decode<T, NW>), dim3(grid), dim3(kThreads), sh, s, b, a);   \
+        return hipGetLastError();                                                             \
     }
-    return hipGetLastError();
+    EZBCH_CASE(1, 1) EZBCH_CASE(2, 1) EZBCH_CASE(3, 1) EZBCH_CASE(4, 1) EZBCH_CASE(5, 1)
+    EZBCH_CASE(6, 1) EZBCH_CASE(7, 1) EZBCH_CASE(8, 1) EZBCH_CASE(9, 1) EZBCH_CASE(10, 1)
+    EZBCH_CASE(11, 1) EZBCH_CASE(12, 1)
+    EZBCH_CASE(5, 2) EZBCH_CASE(6, 2) EZBCH_CASE(7, 2) EZBCH_CASE(8, 2) EZBCH_CASE(9, 2)
+    EZBCH_CASE(10, 2) EZBCH_CASE(11, 2) EZBCH_CASE(12, 2) EZBCH_CASE(13, 2) EZBCH_CASE(14, 2)
+    EZBCH_CASE(15, 2) EZBCH_CASE(16, 2)
+    EZBCH_CASE(9, 4) EZBCH_CASE(10, 4) EZBCH_CASE(11, 4) EZBCH_CASE(12, 4) EZBCH_CASE(13, 4)
+    EZBCH_CASE(14, 4) EZBCH_CASE(15, 4) EZBCH_CASE(16, 4)
+#undef EZBCH_CASE
+    return hipErrorInvalidValue;
 }
 
 // ---- host --------------------------------------------------------------------------------------
@@ -541,17 +579,30 @@ struct HostBch {
         return true;
     }
 
-    // step[v] = (v x^(E+56) mod g) left-justified: the remainder update for one data byte
-    void step_table(uint64_t (&tab)[256]) const {
-        const unsigned E = ecc_bits;
-        uint64_t gl = 0;
+    unsigned words() const { return ecc_bits <= 64 ? 1 : ecc_bits <= 128 ? 2 : 4; }
+    // step[v] = (v x^(E+8 nw 64-8) mod g) left-justified over nw words (w[0] most significant):
+    // the remainder update for one data byte; laid out [v][word]
+    std::vector<uint64_t> step_table() const {
+        const unsigned E = ecc_bits, nw = words(), W = 64 * nw;
+        std::vector<uint64_t> gl(nw, 0), tab(256 * nw);
         for (unsigned i = 0; i < E; ++i)
-            if (g[i]) gl |= 1ull << (64 - E + i);
+            if (g[i]) {
+                const unsigned bit = W - E + i;                  // from the LSB of the whole
+                gl[nw - 1 - bit / 64] |= 1ull << (bit % 64);
+            }
         for (unsigned v = 0; v < 256; ++v) {
-            uint64_t c = (uint64_t)v << 56;
-            for (int k = 0; k < 8; ++k) c = (c >> 63) ? (c << 1) ^ gl : (c << 1);
-            tab[v] = c;
+            std::vector<uint64_t> c(nw, 0);
+            c[0] = (uint64_t)v << 56;
+            for (int k = 0; k < 8; ++k) {
+                const bool top = c[0] >> 63;
+                for (unsigned i = 0; i < nw; ++i)
+                    c[i] = (c[i] << 1) | (i + 1 < nw ? c[i + 1] >> 63 : 0);
+                if (top)
+                    for (unsigned i = 0; i < nw; ++i) c[i] ^= gl[i];
+            }
+            for (unsigned i = 0; i < nw; ++i) tab[v * nw + i] = c[i];
         }
+        return tab;
     }
 };
 
@@ -586,8 +637,8 @@ int create_impl(ezbch_codec **out, unsigned m, unsigned t, unsigned poly, int de
         g_err = "BCH<N,K,T>: K does not match the codec init_bch builds (N - ecc_bits)";
         return -EINVAL;
     }
-    if (t > (unsigned)kMaxT || m * t > 64) {
-        g_err = "BCH device path supports t <= 8 and m*t <= 64";
+    if (t > (unsigned)kMaxT || h.ecc_bits > 64u * kMaxNW) {
+        g_err = "BCH device path supports t <= 16 and ecc_bits <= 256";
         return -ENOTSUP;
     }
     int ndev = 0;
@@ -601,12 +652,11 @@ int create_impl(ezbch_codec **out, unsigned m, unsigned t, unsigned poly, int de
     c->device = device;
     c->h = std::move(h);
     DeviceGuard dg(device);
-    uint64_t tab[256];
-    c->h.step_table(tab);
+    const std::vector<uint64_t> tab = c->h.step_table();
     const size_t nt = c->h.ex.size() + c->h.lg.size();
-    if ((e = hipMalloc(&c->d_step, sizeof tab)) != hipSuccess ||
+    if ((e = hipMalloc(&c->d_step, tab.size() * 8)) != hipSuccess ||
         (e = hipMalloc(&c->d_tabs, nt * sizeof(uint16_t))) != hipSuccess ||
-        (e = hipMemcpy(c->d_step, tab, sizeof tab, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(c->d_step, tab.data(), tab.size() * 8, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(c->d_tabs, c->h.ex.data(), c->h.ex.size() * 2, hipMemcpyHostToDevice)) !=
             hipSuccess ||
         (e = hipMemcpy(c->d_tabs + c->h.ex.size(), c->h.lg.data(), c->h.lg.size() * 2,
@@ -621,7 +671,11 @@ int create_impl(ezbch_codec **out, unsigned m, unsigned t, unsigned poly, int de
     d.ecc_bits = (int)c->h.ecc_bits;
     d.ecc_bytes = (int)c->h.ecc_bytes;
     d.lds_tabs = m <= 12;
-    d.emask = ~0ull << (64 - c->h.ecc_bits);
+    d.nw = (int)c->h.words();
+    for (int i = 0; i < kMaxNW; ++i) {
+        const int hi = (int)c->h.ecc_bits - 64 * i;             // significant bits in word i
+        d.emask[i] = hi >= 64 ? ~0ull : hi <= 0 ? 0ull : ~0ull << (64 - hi);
+    }
     d.step = c->d_step;
     d.ex = c->d_tabs;
     d.lg = c->d_tabs + c->h.ex.size();

@@ -30,7 +30,9 @@ def _flip(rows, nbits, counts, rng):
 
 
 # (m, t): L <= 4 closed-form roots, L > 4 Chien, LDS and global field tables, unused ECC bits
-CODECS = [(5, 2), (8, 2), (8, 8), (10, 4), (11, 5), (12, 5), (13, 4), (15, 4), (7, 8)]
+CODECS = [(5, 2), (8, 2), (8, 8), (10, 4), (11, 5), (12, 5), (13, 4), (15, 4), (7, 8),
+          # beyond one 64-bit remainder word and t > 8 (general BCH)
+          (13, 8), (10, 9), (14, 12), (15, 16), (12, 16), (6, 10), (9, 13), (16 - 1, 9)]
 
 
 @pytest.mark.parametrize("m,t", CODECS, ids=[f"m{m}t{t}" for m, t in CODECS])
