@@ -64,6 +64,7 @@ struct BchArgs {
     size_t lstride;
     size_t ncw;
     int staged;               // the block's data rows are copied to LDS with coalesced loads
+    int ecc_only;             // decode_bch's "ecc = recv XOR calc" form: no data, nothing corrected
 };
 
 constexpr size_t kLdsLimit = 65536;
@@ -433,15 +434,21 @@ template <int T, int NW>
 __global__ void __launch_bounds__(kThreads) k_bch_decode(DevBch b, BchArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     stage_tables(b, smem, true);
-    const uint8_t *row = block_rows(smem, b, true, a);
+    const uint8_t *row = a.ecc_only ? nullptr : block_rows(smem, b, true, a);
     const size_t k = (size_t)blockIdx.x * kThreads + threadIdx.x;
     if (k >= a.ncw) return;
     if (8ull * a.len > (unsigned long long)(b.n - b.ecc_bits)) {   // decode_bch's length check
         a.result[k] = -kEINVAL;
         return;
     }
-    uint8_t *d = a.wdata + k * a.dstride, *e = a.ecc + k * a.estride;
-    Rem<NW> r = data_remainder<NW>(reinterpret_cast<const uint64_t *>(smem), row, a.len);
+    uint8_t *d = a.ecc_only ? nullptr : a.wdata + k * a.dstride, *e = a.ecc + k * a.estride;
+    Rem<NW> r;
+    if (a.ecc_only) {
+#pragma unroll
+        for (int i = 0; i < NW; ++i) r.w[i] = 0;
+    } else {
+        r = data_remainder<NW>(reinterpret_cast<const uint64_t *>(smem), row, a.len);
+    }
     for (int i = 0; i < b.ecc_bytes; ++i) r.w[i >> 3] ^= (uint64_t)e[i] << (56 - 8 * (i & 7));
     uint64_t any = 0;
 #pragma unroll
@@ -462,6 +469,7 @@ __global__ void __launch_bounds__(kThreads) k_bch_decode(DevBch b, BchArgs a) {
         if (i < cnt) {
             const uint32_t el = loc[i];
             if (a.errloc) a.errloc[k * a.lstride + i] = el;
+            if (a.ecc_only) continue;
             if (el < 8u * a.len) d[el >> 3] ^= (uint8_t)(1u << (el & 7));
             else e[(el >> 3) - a.len] ^= (uint8_t)(1u << (el & 7));
         }
@@ -480,7 +488,7 @@ hipError_t launch_encode(const DevBch &b, BchArgs a, hipStream_t s) {
 
 hipError_t launch_decode(const DevBch &b, BchArgs a, hipStream_t s) {
     const unsigned grid = (unsigned)((a.ncw + kThreads - 1) / kThreads);
-    a.staged = want_staging(b, true, a);
+    a.staged = a.ecc_only ? 0 : want_staging(b, true, a);
     const size_t sh = lds_bytes(b, true, a);
     // (T, NW) instantiations: NW = 1 for ecc_bits <= 64 (t <= 12 since m >= 5), NW = 2 for
     // ecc_bits <= 128 (m t > 64: t >= 5), NW = 4 for ecc_bits <= 256 (t >= 9)
@@ -798,7 +806,22 @@ int ezbch_decode(const ezbch_codec *c, uint8_t *data, size_t data_stride, unsign
     if (int r = check_args(c, data, data_stride, len, ecc, ecc_stride, ncw)) return r;
     if (errloc && ncw > 1 && errloc_stride < c->h.t) return -EINVAL;
     DeviceGuard g(c->device);
-    BchArgs a{data, data, data_stride, len, ecc, ecc_stride, result, errloc, errloc_stride, ncw, 0};
+    BchArgs a{data, data, data_stride, len, ecc, ecc_stride, result, errloc, errloc_stride, ncw, 0, 0};
+    hipError_t e = launch_decode(c->dev, a, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? 0 : hip_fail(e, "BCH decode launch");
+}
+
+int ezbch_decode_ecc(const ezbch_codec *c, const uint8_t *ecc, size_t ecc_stride, unsigned len,
+                     int32_t *result, uint32_t *errloc, size_t errloc_stride, size_t ncw,
+                     void *stream) {
+    if (!c) return -EINVAL;
+    if (ncw == 0) return 0;
+    if (!result || !ecc) return -EINVAL;
+    if (ncw > 1 && ecc_stride < c->h.ecc_bytes) return -EINVAL;
+    if (errloc && ncw > 1 && errloc_stride < c->h.t) return -EINVAL;
+    DeviceGuard g(c->device);
+    BchArgs a{nullptr, nullptr, 0, len, const_cast<uint8_t *>(ecc), ecc_stride, result, errloc,
+              errloc_stride, ncw, 0, 1};
     hipError_t e = launch_decode(c->dev, a, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? 0 : hip_fail(e, "BCH decode launch");
 }

@@ -285,6 +285,7 @@ constexpr int kErrWaves = 16;
 constexpr int kErrScratch = 64 + 3 * 32;   // dwords per wave
 constexpr unsigned kExt = 8192;            // antilog entries past NN (lazy reduction)
 constexpr unsigned kSeg = 1025;            // Chien positions per lane (64 kSeg >= 65535, odd)
+constexpr unsigned kHalf = (kSeg + 1) / 2; // second interleaved stream of a lane's segment
 
 __device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
 #pragma unroll
@@ -384,43 +385,53 @@ __global__ void __launch_bounds__(64 * kErrWaves) k_wide_errors(ErrArgs ea) {
             if (lane == 0) a.result[k] = -1;
             continue;
         }
-        // Chien search (1555-1584): lane l walks positions i = 1 + l S + t, t = 0..S-1 (S = kSeg,
-        // odd): reg_j = lambda_j + j i.  Lanes 1025 positions apart spread every term's table reads
-        // over the LDS banks (j i mod 2^16 - 1 rotates the position bits); the table is extended
-        // by kExt entries, so reg_j is reduced only every 256 steps, and a zero coefficient is a
-        // mask, not a branch.  Roots are collected unordered and sorted below (the reference's
-        // ascending-i order).
-        const unsigned seg = kSeg;
-        const unsigned i_l = 1 + lane * seg;
-        unsigned rg[kMaxNR + 1], msk[kMaxNR + 1];
+        // Chien search (1555-1584): lane l walks its segment of S = kSeg positions
+        // [1 + l S, 1 + (l+1) S) as two interleaved halves, i = 1 + l S + t and i + kHalf
+        // (two independent table-read streams per step); reg_j = lambda_j + j i.  The table is
+        // extended by kExt entries, so reg_j is reduced only every 256 steps, and a zero
+        // coefficient is a mask, not a branch.  Roots are collected unordered and sorted below
+        // (the reference's ascending-i order).
+        const unsigned i_a = 1 + lane * kSeg, i_b = i_a + kHalf;
+        unsigned ra[kMaxNR + 1], rb[kMaxNR + 1], msk[kMaxNR + 1];
 #pragma unroll
         for (int j = 1; j <= kMaxNR; ++j) {
             const unsigned lj = __shfl(llog, j, 64);
             msk[j] = (lj != A0 && j <= (int)deg) ? 0xFFFFFFFFu : 0u;   // wave-uniform
-            rg[j] = fold(lj + j * i_l, NN, MM);
+            ra[j] = fold(lj + j * i_a, NN, MM);
+            rb[j] = fold(lj + j * i_b, NN, MM);
         }
         count = 0;
-        for (unsigned t = 0; t < seg; ++t) {
-            unsigned qv = 1;
+        for (unsigned t = 0; t < kHalf; ++t) {
+            unsigned qa = 1, qb = 1;
 #pragma unroll
             for (int j0 = 1; j0 <= kMaxNR; j0 += 4) {
                 if (j0 > (int)deg) break;                    // wave-uniform
 #pragma unroll
                 for (int j = j0; j < j0 + 4; ++j) {
-                    qv ^= AT[rg[j]] & msk[j];
-                    rg[j] += j;
+                    qa ^= AT[ra[j]] & msk[j];
+                    qb ^= AT[rb[j]] & msk[j];
+                    ra[j] += j;
+                    rb[j] += j;
                 }
             }
             if ((t & 255) == 255) {
 #pragma unroll
-                for (int j = 1; j <= kMaxNR; ++j) rg[j] = red1(rg[j], NN);
+                for (int j = 1; j <= kMaxNR; ++j) {
+                    ra[j] = red1(ra[j], NN);
+                    rb[j] = red1(rb[j], NN);
+                }
             }
-            const unsigned i = i_l + t;
-            const uint64_t hit = __ballot(qv == 0 && i <= NN);
-            if (hit) {
-                const unsigned before = __builtin_popcountll(hit & ((1ull << lane) - 1));
-                if (qv == 0 && i <= NN && count + before < kMaxNR + 1) roots[count + before] = i;
-                count += __builtin_popcountll(hit);
+            const unsigned ia = i_a + t, ib = i_b + t;
+            const bool ha = qa == 0 && ia <= NN, hb = qb == 0 && t + kHalf < kSeg && ib <= NN;
+            const uint64_t hit_a = __ballot(ha), hit_b = __ballot(hb);
+            if (hit_a | hit_b) {
+                const uint64_t below = (1ull << lane) - 1;
+                const unsigned na = __builtin_popcountll(hit_a);
+                if (ha && count + __builtin_popcountll(hit_a & below) < kMaxNR + 1)
+                    roots[count + __builtin_popcountll(hit_a & below)] = ia;
+                if (hb && count + na + __builtin_popcountll(hit_b & below) < kMaxNR + 1)
+                    roots[count + na + __builtin_popcountll(hit_b & below)] = ib;
+                count += na + __builtin_popcountll(hit_b);
                 if (count >= (int)deg) break;
             }
         }

@@ -94,6 +94,7 @@ def lib():
         L.ezbch_encode_rows.argtypes = [_vp, _vp, _sz, _u, _sz, _vp]
         L.ezbch_encode_rows_host.argtypes = [_vp, _vp, _sz, _u, _sz, _sz]
         L.ezbch_decode.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _vp, _vp, _sz, _sz, _vp]
+        L.ezbch_decode_ecc.argtypes = [_vp, _vp, _sz, _u, _vp, _vp, _sz, _sz, _vp]
         L.ezbch_encode_host.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _sz, _sz]
         L.ezbch_decode_host.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _vp, _vp, _sz, _sz, _sz]
         _lib = L
@@ -385,6 +386,20 @@ class BCH:
         _dev_rows(result, "result", self.device, 4, ndim=1)
         _check(lib().ezbch_decode(self._h, _tp(data), ds, length, _tp(ecc), es, _tp(result),
                                   _tp(errloc), ls, ncw, _stream_ptr(stream)), "ezbch_decode", True)
+        return result
+
+    def decode_ecc(self, ecc, length, result=None, errloc=None, stream=None):
+        """decode_bch's recv XOR calc form: ecc rows hold the ECC differences; returns the int32
+        results (errors found, or a negative errno); nothing is corrected (ezbch_decode_ecc)."""
+        import torch
+        ncw = ecc.shape[0]
+        es = _dev_rows(ecc, "ecc", self.device, 1)
+        ls = _dev_rows(errloc, "errloc", self.device, 4)
+        if result is None:
+            result = torch.empty(ncw, dtype=torch.int32, device=ecc.device)
+        _dev_rows(result, "result", self.device, 4, ndim=1)
+        _check(lib().ezbch_decode_ecc(self._h, _tp(ecc), es, length, _tp(result), _tp(errloc), ls,
+                                      ncw, _stream_ptr(stream)), "ezbch_decode_ecc", True)
         return result
 
     def encode_host(self, data, length=None, ecc=None, chunk=0):

@@ -69,6 +69,14 @@ int ezbch_decode(const ezbch_codec *codec, uint8_t *data, size_t data_stride, un
                  uint8_t *ecc, size_t ecc_stride, int32_t *result, uint32_t *errloc,
                  size_t errloc_stride, size_t ncw, void *stream);
 
+/* decode_bch's "ecc = recv_ecc XOR calc_ecc" form (bch_base:96-111, Djelic's decode without the
+ * data): for every codeword k < ncw, result[k] = the number of errors the ECC difference ecc_k
+ * reveals for a codeword of len data bytes (or -EBADMSG / -EINVAL), with the error locations in
+ * errloc; nothing is corrected and no data is read.  Device pointers. */
+int ezbch_decode_ecc(const ezbch_codec *codec, const uint8_t *ecc, size_t ecc_stride, unsigned len,
+                     int32_t *result, uint32_t *errloc, size_t errloc_stride, size_t ncw,
+                     void *stream);
+
 /* Host-memory forms (blocking), streamed through the device in chunks of `chunk` codewords
  * (0 = library default).  Encode moves only the data bytes in and a compact ECC block out; the
  * caller's data bytes are never written. */

@@ -163,3 +163,32 @@ def test_c5_full_size_round_trip(torch):
     res = c.decode(d, L).cpu().numpy()
     np.testing.assert_array_equal(res, counts)
     assert torch.equal(d, rows)
+
+
+@pytest.mark.parametrize("m,t", [(10, 4), (13, 8), (15, 16)])
+def test_decode_from_ecc_difference(torch, m, t):
+    """decode_bch's recv XOR calc form (bch_base:96-111; ezbch_decode_ecc): the locations found
+    from the ECC difference alone equal those of a full decode of the same corrupted codeword."""
+    import ezrs
+    oc, c = O.BCH(m, t), ezrs.BCH(m, t)
+    rng = np.random.default_rng(7 * m + t)
+    L, ncw, eb = min(oc.max_len, 200), 3000, oc.ecc_bytes
+    ref = rng.integers(0, 256, (ncw, L + eb), dtype=np.uint8)
+    oc.encode_batch(ref, L)
+    bad = ref.copy()
+    _flip(bad, 8 * L + oc.ecc_bits, np.arange(ncw) % (t + 3), rng)
+    exp = bad.copy()
+    eloc = np.zeros((ncw, t), np.uint32)
+    eres = oc.decode_batch(exp, L, errloc=eloc)
+    # calc_ecc = ECC of the received data; the difference with the received ECC
+    calc = bad.copy()
+    oc.encode_batch(calc, L)
+    diff = (calc[:, L:] ^ bad[:, L:]).copy()
+    d = torch.from_numpy(diff).cuda()
+    loc = torch.zeros((ncw, t), dtype=torch.int32, device="cuda")
+    res = c.decode_ecc(d, L, errloc=loc).cpu().numpy()
+    np.testing.assert_array_equal(res, eres)
+    got = loc.cpu().numpy().view(np.uint32)
+    for k in np.nonzero(eres > 0)[0]:
+        np.testing.assert_array_equal(got[k, :eres[k]], eloc[k, :eres[k]])
+    np.testing.assert_array_equal(d.cpu().numpy(), diff)        # nothing corrected
