@@ -165,18 +165,31 @@ def gen_codec(m, poly, fcr, prim, nr):
         f"C{m}_{poly:x}_{fcr}_{prim}_{nr}"
     out = [f"// ---- {tag}: m={m} poly={poly:#x} fcr={fcr} prim={prim} nroots={nr}: "
            f"{len(lead)} coset leaders ----"]
-    costs = []
-    for li, e in enumerate(lead):
+    # slot order: waves take slots (2w, 2w+1); pair the costliest networks with the cheapest so
+    # that the waves of a workgroup reach each window's barrier together
+    cost = {}
+    for e in lead:
         mp, d = min_poly(gf, e)
         assert d == m, f"leader {e}: degree {d}"
+        cost[e] = gen_block("x", mp, d)[1]
+    by = sorted(lead, key=lambda e: (-cost[e], e))
+    order = []
+    while by:
+        order.append(by.pop(0))
+        if by:
+            order.append(by.pop())
+    costs = []
+    for li, e in enumerate(order):
+        mp, d = min_poly(gf, e)
         body, ops = gen_block(f"wb_{tag}_{li}", mp, d)
         costs.append(ops)
-        out.append(f"// leader {e}: M(x) = {mp:#x}, {ops} ops per 16-symbol block")
+        out.append(f"// slot {li}: leader {e}: M(x) = {mp:#x}, {ops} ops per 16-symbol block")
         out += body
-    nl = len(lead)
+    nl = len(order)
     out.append(f"struct WC_{tag} {{")
     out.append(f"    static constexpr unsigned M = {m}, POLY = {poly:#x}, FCR = {fcr}, PRIM = {prim}, NR = {nr};")
     out.append(f"    static constexpr int NL = {nl};")
+    out.append(f"    static constexpr uint16_t LEADER[{nl}] = {{{', '.join(str(e) for e in order)}}};  // slot -> coset leader")
     out.append("    template <int L>")
     out.append("    static __device__ __forceinline__ void block(uint32_t (&s)[16], const uint32_t (&c)[16]) {")
     for li in range(nl):

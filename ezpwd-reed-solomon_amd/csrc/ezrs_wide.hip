@@ -30,6 +30,9 @@ constexpr int kWin = 128;                   // symbols per window
 constexpr int kRowBytes = 2 * kWin;         // 256 B of each row per window
 constexpr int kBuf = kRows * kRowBytes;     // 32 KiB
 constexpr int kLPW = 2;                     // leaders per wave
+constexpr int kNBuf = 2;                    // window ring: the DMA runs kNBuf - 1 windows ahead
+// (measured alternatives, C4 k_wide_rem per launch: 2 leaders x 8 waves, 2 buffers, 2 workgroups
+// per CU 3.8 ms; 1 leader x 16 waves, 3 buffers, 1 workgroup per CU 4.7 ms)
 constexpr int kMaxNR = 32;
 constexpr int32_t kSentinel = INT32_MIN;
 
@@ -94,6 +97,7 @@ __device__ __forceinline__ void rem_body(const RemArgs &a, uint8_t *lds, int lan
         }
     };
 
+    constexpr int IPW = 32 / NW;                       // DMA instructions per wave per window
     uint32_t S[kLPW][16];
 #pragma unroll
     for (int L = 0; L < kLPW; ++L)
@@ -102,12 +106,17 @@ __device__ __forceinline__ void rem_body(const RemArgs &a, uint8_t *lds, int lan
 
     const uint32_t p = (uint32_t)lane, q = (p >> 3) & 1;
     const uint32_t rowa = lbuf + 2 * p * kRowBytes;
-    issue(0, 0);
+    for (uint32_t w = 0; w + 1 < (uint32_t)kNBuf && w < nwin; ++w) issue(w, w);
     for (uint32_t w = 0; w < nwin; ++w) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();                                   // window w landed; buffer w+1 is free
-        if (w + 1 < nwin) issue(w + 1, (w + 1) & 1);
-        const uint32_t wb = rowa + (w & 1) * kBuf;
+        // window w landed (this wave's share: all but the younger windows' DMA), then every
+        // wave's share (barrier); the buffer of window w - 1 is free for window w + kNBuf - 1
+        if (w + kNBuf - 2 < nwin)
+            asm volatile("s_waitcnt vmcnt(%0)" :: "n"(IPW * (kNBuf - 2)) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (w + kNBuf - 1 < nwin) issue(w + kNBuf - 1, (w + kNBuf - 1) % kNBuf);
+        const uint32_t wb = rowa + (w % kNBuf) * kBuf;
         if (w == 0 && z) {
             // positions before the row's start (the previous row's bytes, or zeros): clear them in
             // this lane's two rows (every wave writes the same zeros, each before its own reads)
@@ -133,6 +142,8 @@ __device__ __forceinline__ void rem_body(const RemArgs &a, uint8_t *lds, int lan
                 }
             }
         }
+        // (LDS reads as inline asm with the wait per block: the compiler-scheduled form that
+        // loads block b + 1 during block b measured slower, 4.09 vs 3.83 ms per C4 launch)
 #pragma unroll
         for (int b = 0; b < 8; ++b) {
             const uint32_t blk = wb + 32 * ((uint32_t)b ^ (p & 7));
@@ -154,7 +165,7 @@ __device__ __forceinline__ void rem_body(const RemArgs &a, uint8_t *lds, int lan
                 c[2 * t + 1] = __builtin_amdgcn_perm(rb[t], ra[t], 0x07060302u);
             }
             C::template block<kLPW * W>(S[0], c);
-            if constexpr (kLPW * W + 1 < C::NL) C::template block<kLPW * W + 1>(S[1], c);
+            if constexpr (kLPW == 2 && kLPW * W + 1 < C::NL) C::template block<kLPW * W + 1>(S[kLPW - 1], c);
         }
     }
     // remainders of the lane's two codewords (low halves: row 2p, high halves: row 2p + 1)
@@ -176,22 +187,22 @@ __device__ __forceinline__ void rem_body(const RemArgs &a, uint8_t *lds, int lan
     }
 }
 
+// wave -> rem_body<C, W> (the leader set is a template parameter: wave-uniform networks)
+template <class C, int NW, int W = 0>
+__device__ __forceinline__ void static_for_waves(const RemArgs &a, uint8_t *lds, int lane, int wave) {
+    if constexpr (W < NW) {
+        if (wave == W) rem_body<C, W>(a, lds, lane);
+        else static_for_waves<C, NW, W + 1>(a, lds, lane, wave);
+    }
+}
+
 template <class C>
 __global__ void __launch_bounds__(64 * ((C::NL + kLPW - 1) / kLPW)) k_wide_rem(RemArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kBuf];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kNBuf * kBuf];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     constexpr int NW = (C::NL + kLPW - 1) / kLPW;
-    static_assert(NW <= 8, "at most 16 leaders");
-    switch (wave) {
-    case 0: rem_body<C, 0>(a, lds, lane); break;
-    case 1: if constexpr (NW > 1) rem_body<C, 1>(a, lds, lane); break;
-    case 2: if constexpr (NW > 2) rem_body<C, 2>(a, lds, lane); break;
-    case 3: if constexpr (NW > 3) rem_body<C, 3>(a, lds, lane); break;
-    case 4: if constexpr (NW > 4) rem_body<C, 4>(a, lds, lane); break;
-    case 5: if constexpr (NW > 5) rem_body<C, 5>(a, lds, lane); break;
-    case 6: if constexpr (NW > 6) rem_body<C, 6>(a, lds, lane); break;
-    default: if constexpr (NW > 7) rem_body<C, 7>(a, lds, lane); break;
-    }
+    static_assert(NW <= 16 && 32 % NW == 0, "waves must split the window's 32 DMA instructions");
+    static_for_waves<C, NW>(a, lds, lane, wave);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -585,8 +596,15 @@ bool wide_build_consts(int id, const CodecMath &m, std::vector<uint16_t> &blob) 
     const unsigned NN = m.nn, NR = m.spec.nroots;
     if (NR > wide::kMaxNR) return false;
     const Field &gf = m.gf;
-    // leaders in order of first appearance
+    // the kernel's slot order of the coset leaders (gen_wide.py: WC_*::LEADER)
     std::vector<unsigned> lead;
+    {
+        int k = 0;
+#define EZRS_WIDE_LEAD(C) \
+        if (k++ == id) lead.assign(wide::WC_##C::LEADER, wide::WC_##C::LEADER + wide::WC_##C::NL);
+        EZRS_WIDE_CODEC_LIST(EZRS_WIDE_LEAD)
+#undef EZRS_WIDE_LEAD
+    }
     std::vector<uint8_t> li(NR);
     std::vector<uint16_t> el(NR);
     for (unsigned i = 0; i < NR; ++i) {
@@ -596,7 +614,7 @@ bool wide_build_consts(int id, const CodecMath &m, std::vector<uint16_t> &blob) 
         do { x = (unsigned)((2ull * x) % NN); if (x < mn) mn = x; } while (x != e);
         unsigned slot = 0;
         while (slot < lead.size() && lead[slot] != mn) ++slot;
-        if (slot == lead.size()) lead.push_back(mn);
+        if (slot == lead.size()) return false;          // not a coset the kernel evaluates
         li[i] = (uint8_t)slot;
     }
     // V[i][k] = beta_i^(NR-1-k); invert by Gauss-Jordan
@@ -642,7 +660,6 @@ bool wide_build_consts(int id, const CodecMath &m, std::vector<uint16_t> &blob) 
             const unsigned q = gf.mul(Inv[k * NR + i], bn);
             blob[2 * wide::kMaxNR + k * NR + i] = (uint16_t)(q ? gf.index_of[q] : NN);
         }
-    (void)id;
     return true;
 }
 
