@@ -267,6 +267,38 @@ def test_c2_c3_full_size(torch):
     assert torch.equal(pos[:, :12], exp_pos)
 
 
+def test_c2_past_infinity_cache(torch):
+    """4M RS(255,223) codewords (1.07 GB, past the 256 MiB Infinity Cache): parity equals the oracle
+    on rows sampled across the whole batch (every tile and launch chunk boundary region), clean
+    decode returns 0 everywhere, and 8 errors per codeword spread over the batch decode back to
+    the original rows."""
+    import ezrs
+    c = ezrs.Codec.rs(255, 223)
+    oc = O.Codec(*O.rs_params(255, 223))
+    ncw = 4 << 20
+    gen = torch.Generator(device="cuda").manual_seed(0x5EED0004)
+    cw = torch.randint(0, 256, (ncw, 255), generator=gen, device="cuda", dtype=torch.int32)
+    cw = cw.to(torch.uint8)
+    c.encode(cw, 223)
+    torch.cuda.synchronize()
+    idx = np.unique(np.concatenate([np.arange(0, ncw, 997), np.arange(ncw - 300, ncw),
+                                    np.arange(0, 300)]))
+    sample = cw[torch.from_numpy(idx).cuda()].cpu().numpy()
+    exp = sample.copy()
+    oc.encode_batch(exp, 223, None, nthreads=8)
+    np.testing.assert_array_equal(sample, exp)
+    clean = cw.clone()
+    r = c.decode(clean, 223)
+    torch.cuda.synchronize()
+    assert int((r != 0).sum()) == 0 and torch.equal(clean, cw)
+    bad = cw.clone()
+    _inject(torch, bad, 8, 0, 255, gen)
+    r = c.decode(bad, 223)
+    torch.cuda.synchronize()
+    assert int((r != 8).sum()) == 0
+    assert torch.equal(bad, cw)
+
+
 @pytest.mark.parametrize("maker", ["RS(255,223)", "RS_CCSDS(255,223)", "RS_CCSDS_CONV(255,223)",
                                    "RS(255,239)", "RS(255,251)"])
 @pytest.mark.parametrize("L,ncw,extra", [(1, 1, 0), (2, 511, 3), (63, 513, 0), (64, 777, 5),
