@@ -14,9 +14,9 @@
 //                  Decode: result 0 for a codeword with zero syndromes and no erasures
 //                  (rs_base:1416-1434); the others get queued for
 //   k_wide_errors  one wavefront per flagged codeword: erasure locator + Berlekamp-Massey with the
-//                  discrepancy as a wave reduction (rs_base:1436-1546), Chien search over all NN
-//                  positions spread over the 64 lanes with alpha_to in LDS, roots kept in the
-//                  reference's ascending order by ballot + prefix count (1548-1584), Omega and
+//                  discrepancy as a wave reduction (rs_base:1436-1546), the roots the Chien search
+//                  would find (1548-1584) by Berlekamp's trace algorithm over lane-parallel
+//                  polynomials with alpha_to in LDS, sorted to the reference's order, Omega and
 //                  Forney per root lane (1589-1690), the reference's partial-correction-on-failure
 //                  semantics, positions in the pad-relative frame (1713-1716).
 #include "ezrs_internal.hpp"
@@ -34,6 +34,7 @@ constexpr int kNBuf = 2;                    // window ring: the DMA runs kNBuf -
 // (measured alternatives, C4 k_wide_rem per launch: 2 leaders x 8 waves, 2 buffers, 2 workgroups
 // per CU 3.8 ms; 1 leader x 16 waves, 3 buffers, 1 workgroup per CU 4.7 ms)
 constexpr int kMaxNR = 32;
+constexpr int kM = 16;                      // symbol bits of every wide codec
 constexpr int32_t kSentinel = INT32_MIN;
 
 typedef int rsrc_t __attribute__((ext_vector_type(4)));
@@ -290,13 +291,14 @@ struct ErrArgs {
     DecodeArgs d;
     const uint16_t *syn;
     const uint32_t *queue;
+    uint32_t stop;              // PHASE EXPERIMENT
+    uint16_t qsolve[16];        // y = sum_j c_j qsolve[j] solves y^2 + y = c when Tr(c) = 0
 };
 
 constexpr int kErrWaves = 16;
-constexpr int kErrScratch = 64 + 3 * 32;   // dwords per wave
-constexpr unsigned kExt = 8192;            // antilog entries past NN (lazy reduction)
-constexpr unsigned kSeg = 1025;            // Chien positions per lane (64 kSeg >= 65535, odd)
-constexpr unsigned kHalf = (kSeg + 1) / 2; // second interleaved stream of a lane's segment
+// per-wave scratch, dwords: roots 64, omega/syndromes/lambda 3 x 32, factor pool 32 (64 u16),
+// factor stack 40
+constexpr int kErrScratch = 64 + 3 * 32 + 32 + 40;
 
 __device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
 #pragma unroll
@@ -313,6 +315,74 @@ __device__ __forceinline__ unsigned fold(unsigned x, unsigned nn, unsigned mm) {
     return red1(x, nn);
 }
 
+// ---- lane-parallel polynomials over GF(2^m): lane j holds coefficient j (degree <= 63) ----------
+struct Gf {
+    const uint16_t *AT;     // antilog, LDS
+    const uint16_t *I;      // log, global
+    unsigned nn;
+};
+
+__device__ __forceinline__ int pdeg(unsigned a) {
+    const uint64_t nz = __ballot(a != 0);
+    return nz ? 63 - __builtin_clzll(nz) : -1;
+}
+__device__ __forceinline__ unsigned plog(const Gf &g, unsigned a) { return a ? g.I[a] : g.nn; }
+__device__ __forceinline__ unsigned pexp(const Gf &g, unsigned l) { return l != g.nn ? g.AT[l] : 0u; }
+
+// a mod b: b monic of degree db >= 1 given in log form (blog), a of degree <= da
+__device__ unsigned pmod(const Gf &g, unsigned a, int da, unsigned blog, int db, unsigned lane) {
+    for (int t = da; t >= db; --t) {
+        const unsigned c = __builtin_amdgcn_readlane(a, t);
+        const unsigned bl = __shfl(blog, (int)((lane - (unsigned)(t - db)) & 63), 64);
+        if (c) {
+            const unsigned lc = __builtin_amdgcn_readfirstlane(g.I[c]);
+            if ((int)lane >= t - db && (int)lane <= t && bl != g.nn) a ^= g.AT[red1(lc + bl, g.nn)];
+        }
+    }
+    return a;
+}
+
+// log form of a / a[d]
+__device__ __forceinline__ unsigned pmonic_log(const Gf &g, unsigned a, int d) {
+    const unsigned lc = __builtin_amdgcn_readfirstlane(g.I[__builtin_amdgcn_readlane(a, d)]);
+    const unsigned al = plog(g, a);
+    return al != g.nn ? red1(al + g.nn - lc, g.nn) : g.nn;
+}
+
+// monic gcd(a, b) (polynomial form), its degree in dg; a != 0
+__device__ unsigned pgcd(const Gf &g, unsigned a, unsigned b, int &dg, unsigned lane) {
+    int da = pdeg(a), db = pdeg(b);
+    if (db < 0) {                                    // gcd(a, 0) = a / a[da]
+        dg = da;
+        return pexp(g, pmonic_log(g, a, da));
+    }
+    while (db >= 0) {
+        const unsigned bl = pmonic_log(g, b, db);
+        const unsigned r = db > 0 ? pmod(g, a, da, bl, db, lane) : 0u;
+        a = pexp(g, bl);
+        da = db;
+        b = r;
+        db = pdeg(r);
+    }
+    dg = da;
+    return a;
+}
+
+// f / gm for gm | f, gm monic of degree dg in log form
+__device__ unsigned pdiv(const Gf &g, unsigned f, int df, unsigned gl, int dg, unsigned lane) {
+    unsigned q = 0;
+    for (int t = df; t >= dg; --t) {
+        const unsigned c = __builtin_amdgcn_readlane(f, t);
+        const unsigned bl = __shfl(gl, (int)((lane - (unsigned)(t - dg)) & 63), 64);
+        if (c) {
+            const unsigned lc = __builtin_amdgcn_readfirstlane(g.I[c]);
+            if ((int)lane == t - dg) q = c;
+            if ((int)lane >= t - dg && (int)lane <= t && bl != g.nn) f ^= g.AT[red1(lc + bl, g.nn)];
+        }
+    }
+    return q;
+}
+
 __global__ void __launch_bounds__(64 * kErrWaves) k_wide_errors(ErrArgs ea) {
     extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
     const DevCodec &c = ea.c;
@@ -320,17 +390,21 @@ __global__ void __launch_bounds__(64 * kErrWaves) k_wide_errors(ErrArgs ea) {
     const unsigned NN = c.nn, A0 = c.nn, NR = c.nroots, FCR = c.fcr, PRM = c.prim, MM = c.mm;
     const uint32_t nq = ea.queue[0];
     if ((size_t)blockIdx.x * kErrWaves >= nq) return;      // uniform over the workgroup
-    uint16_t *AT = smem;                          // alpha^(e mod NN) for e < NN + kExt (Chien)
-    for (unsigned i = threadIdx.x; i < NN + kExt; i += blockDim.x) AT[i] = c.alpha_to[i < NN ? i : i - NN];
+    uint16_t *AT = smem;                          // alpha^e, e < NN
+    for (unsigned i = threadIdx.x; i < NN; i += blockDim.x) AT[i] = c.alpha_to[i];
     const int wave = threadIdx.x >> 6;
     const unsigned lane = threadIdx.x & 63;
-    // per-wave scratch: roots (u32 x 64), omega, syndromes, lambda (index form, u16 x 64 each)
-    uint32_t *roots = reinterpret_cast<uint32_t *>(smem + ((NN + kExt + 7) & ~7u)) + wave * kErrScratch;
+    // per-wave scratch: roots (u32 x 64), omega, syndromes, lambda (index form, u16 x 64 each),
+    // the root finder's factor pool (u16 x 64) and stack (u32 x 40)
+    uint32_t *roots = reinterpret_cast<uint32_t *>(smem + ((NN + 7) & ~7u)) + wave * kErrScratch;
     uint16_t *omg = reinterpret_cast<uint16_t *>(roots + 64);
     uint16_t *slg = omg + 64;
     uint16_t *llg = slg + 64;
+    uint16_t *pool = llg + 64;
+    uint32_t *stk = reinterpret_cast<uint32_t *>(pool + 64);
     __syncthreads();
     const uint16_t *I = c.index_of;
+    const Gf g{AT, I, NN};
     const unsigned len = a.len, pad = c.load - len;
 
     for (uint32_t qi = blockIdx.x * kErrWaves + wave; qi < nq; qi += gridDim.x * kErrWaves) {
@@ -350,6 +424,7 @@ __global__ void __launch_bounds__(64 * kErrWaves) k_wide_errors(ErrArgs ea) {
         if (!__ballot(sp != 0)) { if (lane == 0) a.result[k] = 0; continue; }   // 1416-1434
         const unsigned sl = sp ? I[sp] : A0;                 // syn[lane], index form
         slg[lane] = (uint16_t)sl;
+        if (ea.stop == 1) { if (lane == 0) a.result[k] = -1; continue; }
 
         // erasure locator (1436-1450): lane j holds lambda[j] (polynomial form)
         unsigned lam = lane == 0 ? 1u : 0u;
@@ -392,58 +467,96 @@ __global__ void __launch_bounds__(64 * kErrWaves) k_wide_errors(ErrArgs ea) {
         const uint64_t nzl = __ballot(lam != 0 && lane <= NR);
         const unsigned deg = 63 - __builtin_clzll(nzl);
         llg[lane] = (uint16_t)llog;
+        if (ea.stop == 2) { if (lane == 0) a.result[k] = -1; continue; }
         if (deg == 0) {                                      // 1577-1595 (no root can match)
             if (lane == 0) a.result[k] = -1;
             continue;
         }
-        // Chien search (1555-1584): lane l walks its segment of S = kSeg positions
-        // [1 + l S, 1 + (l+1) S) as two interleaved halves, i = 1 + l S + t and i + kHalf
-        // (two independent table-read streams per step); reg_j = lambda_j + j i.  The table is
-        // extended by kExt entries, so reg_j is reduced only every 256 steps, and a zero
-        // coefficient is a mask, not a branch.  Roots are collected unordered and sorted below
-        // (the reference's ascending-i order).
-        const unsigned i_a = 1 + lane * kSeg, i_b = i_a + kHalf;
-        unsigned ra[kMaxNR + 1], rb[kMaxNR + 1], msk[kMaxNR + 1];
+        // Roots of lambda -- the set the Chien search finds (1555-1584) -- by Berlekamp's trace
+        // algorithm.  lambda has deg distinct roots in GF(2^m) iff x^(2^m) = x mod lambda
+        // (x^(2^m) - x is the product of all x - a); otherwise the reference's search finds fewer
+        // than deg roots and gives up.  P_k = x^(2^k) mod L (L = lambda made monic) by repeated
+        // squaring; a factor F of L splits as gcd(F, Tr(beta x) mod F), Tr(y) = sum_k y^(2^k),
+        // beta = alpha^b for b = 0..m-1 (a basis: two distinct roots differ in some
+        // Tr(alpha^b .)).  Factors wait on a stack in LDS; a linear factor x + r gives the root
+        // r = alpha^i, i in [1, NN] as the reference numbers positions.
+        const unsigned Ll = pmonic_log(g, lam, (int)deg);
+        const unsigned x1 = deg >= 2 ? (lane == 1 ? 1u : 0u) : (lane == 0 ? pexp(g, Ll) : 0u);
+        unsigned Pl[kM];                                     // log form of P_0 .. P_(m-1)
+        unsigned P = x1;
 #pragma unroll
-        for (int j = 1; j <= kMaxNR; ++j) {
-            const unsigned lj = __shfl(llog, j, 64);
-            msk[j] = (lj != A0 && j <= (int)deg) ? 0xFFFFFFFFu : 0u;   // wave-uniform
-            ra[j] = fold(lj + j * i_a, NN, MM);
-            rb[j] = fold(lj + j * i_b, NN, MM);
+        for (int kk = 0; kk < kM; ++kk) {
+            Pl[kk] = plog(g, P);
+            const unsigned src = __shfl(Pl[kk], (int)(lane >> 1), 64);
+            const unsigned sq = (lane & 1) == 0 && src != A0 ? AT[red1(2 * src, NN)] : 0u;
+            P = pmod(g, sq, 2 * (int)deg - 2, Ll, (int)deg, lane);
         }
-        count = 0;
-        for (unsigned t = 0; t < kHalf; ++t) {
-            unsigned qa = 1, qb = 1;
+        count = __ballot(P != x1) ? -1 : 0;
+        if (ea.stop == 4) { if (lane == 0) a.result[k] = -1; continue; }
+        if (count == 0) {
+            if (lane <= deg) pool[lane] = (uint16_t)pexp(g, Ll);
+            if (lane == 0) stk[0] = deg << 8;                // off | deg << 8 | first b << 16
+            int nstk = 1;
+            __builtin_amdgcn_wave_barrier();
+            while (nstk > 0) {
+                const uint32_t e = stk[--nstk];
+                const int off = (int)(e & 255), f = (int)((e >> 8) & 255);
+                const unsigned F = (int)lane <= f ? pool[off + lane] : 0u;
+                __builtin_amdgcn_wave_barrier();
+                if (f == 2) {
+                    // x^2 + p x + q, p != 0 (distinct roots): x = p y, y^2 + y = q / p^2, a GF(2)-
+                    // linear equation with the precomputed solver; roots p y and p y + p
+                    const unsigned q = __builtin_amdgcn_readlane(F, 0), pp = __builtin_amdgcn_readlane(F, 1);
+                    if (!pp) { count = -1; break; }
+                    const unsigned lp = __builtin_amdgcn_readfirstlane(I[pp]);
+                    const unsigned lq = __builtin_amdgcn_readfirstlane(I[q]);
+                    const unsigned cv = __builtin_amdgcn_readfirstlane(AT[fold(lq + 2 * (NN - lp), NN, MM)]);
+                    unsigned y = 0;
 #pragma unroll
-            for (int j0 = 1; j0 <= kMaxNR; j0 += 4) {
-                if (j0 > (int)deg) break;                    // wave-uniform
-#pragma unroll
-                for (int j = j0; j < j0 + 4; ++j) {
-                    qa ^= AT[ra[j]] & msk[j];
-                    qb ^= AT[rb[j]] & msk[j];
-                    ra[j] += j;
-                    rb[j] += j;
+                    for (int j = 0; j < kM; ++j) y ^= (cv >> j & 1) ? ea.qsolve[j] : 0u;
+                    const unsigned ly = __builtin_amdgcn_readfirstlane(I[y]);
+                    const unsigned r1 = AT[red1(lp + ly, NN)], r2 = r1 ^ pp;
+                    const unsigned i1 = I[lane == 0 ? r1 : r2];
+                    if (lane < 2) roots[count + lane] = i1 ? i1 : NN;
+                    count += 2;
+                    continue;
                 }
-            }
-            if ((t & 255) == 255) {
-#pragma unroll
-                for (int j = 1; j <= kMaxNR; ++j) {
-                    ra[j] = red1(ra[j], NN);
-                    rb[j] = red1(rb[j], NN);
+                if (f == 1) {
+                    const unsigned il = __builtin_amdgcn_readfirstlane(I[__builtin_amdgcn_readlane(F, 0)]);
+                    if (lane == 0) roots[count] = il ? il : NN;
+                    ++count;
+                    continue;
                 }
-            }
-            const unsigned ia = i_a + t, ib = i_b + t;
-            const bool ha = qa == 0 && ia <= NN, hb = qb == 0 && t + kHalf < kSeg && ib <= NN;
-            const uint64_t hit_a = __ballot(ha), hit_b = __ballot(hb);
-            if (hit_a | hit_b) {
-                const uint64_t below = (1ull << lane) - 1;
-                const unsigned na = __builtin_popcountll(hit_a);
-                if (ha && count + __builtin_popcountll(hit_a & below) < kMaxNR + 1)
-                    roots[count + __builtin_popcountll(hit_a & below)] = ia;
-                if (hb && count + na + __builtin_popcountll(hit_b & below) < kMaxNR + 1)
-                    roots[count + na + __builtin_popcountll(hit_b & below)] = ib;
-                count += na + __builtin_popcountll(hit_b);
-                if (count >= (int)deg) break;
+                const unsigned Fl = plog(g, F);              // F is monic
+                bool split = false;
+                for (unsigned b = e >> 16; b < (unsigned)kM; ++b) {
+                    unsigned T = 0, eb = b;                  // Tr(alpha^b x) mod L
+#pragma unroll
+                    for (int kk = 0; kk < kM; ++kk) {
+                        if (Pl[kk] != A0) T ^= AT[red1(Pl[kk] + eb, NN)];
+                        eb = red1(2 * eb, NN);
+                    }
+                    const unsigned R = pmod(g, T, (int)deg - 1, Fl, f, lane);
+                    int dg;
+                    const unsigned G = pgcd(g, F, R, dg, lane);
+                    if (dg > 0 && dg < f) {
+                        const unsigned H = pdiv(g, F, f, plog(g, G), dg, lane);
+                        if ((int)lane <= dg) pool[off + lane] = (uint16_t)G;
+                        if ((int)lane <= f - dg) pool[off + dg + 1 + lane] = (uint16_t)H;
+                        if (lane == 0) {
+                            stk[nstk] = (uint32_t)off | (uint32_t)dg << 8 | (b + 1) << 16;
+                            stk[nstk + 1] = (uint32_t)(off + dg + 1) | (uint32_t)(f - dg) << 8 | (b + 1) << 16;
+                        }
+                        nstk += 2;
+                        __builtin_amdgcn_wave_barrier();
+                        split = true;
+                        break;
+                    }
+                }
+                if (!split) {                                // unreachable for distinct roots
+                    count = -1;
+                    break;
+                }
             }
         }
         if (count == (int)deg) {                             // ascending order (rank sort)
@@ -461,6 +574,7 @@ __global__ void __launch_bounds__(64 * kErrWaves) k_wide_errors(ErrArgs ea) {
             if (lane == 0) a.result[k] = -1;
             continue;
         }
+        if (ea.stop == 3) { if (lane == 0) a.result[k] = -1; continue; }
         // Omega = S Lambda mod x^NR (1596-1604): lane i <= deg - 1
         const unsigned deg_omega = deg - 1;
         if (lane <= deg_omega) {
@@ -521,6 +635,7 @@ __global__ void __launch_bounds__(64 * kErrWaves) k_wide_errors(ErrArgs ea) {
 namespace {
 
 template <class C> bool wide_matches(const DevCodec &d) {
+    static_assert(C::M == wide::kM, "the wide engine is GF(2^16)");
     return d.mm == C::M && d.poly == C::POLY && d.fcr == C::FCR && d.prim == C::PRIM &&
            d.nroots == C::NR && !d.dual && !d.masked;
 }
@@ -592,6 +707,34 @@ size_t wide_ws_bytes(int id, size_t ncw) {
 
 // Host tables of a wide codec: leader of each syndrome (same coset rule as gen_wide.py) and
 // Q = V^-1 diag(beta^NR) in index form.
+// Linear solver of y^2 + y = c over GF(2^mm) (field polynomial poly): y -> y^2 + y is GF(2)-linear
+// with kernel {0, 1}; its image (trace-0 elements) gets a reduced echelon basis b_j (pivot bit j)
+// with preimages p_j, so for c in the image y = sum over pivot bits j of c_j p_j.
+void quad_solver(unsigned poly, unsigned mm, uint16_t out[16]) {
+    auto mul = [&](unsigned a, unsigned b) {
+        unsigned r = 0;
+        for (unsigned i = 0; i < mm; ++i) {
+            if (b >> i & 1) r ^= a;
+            a <<= 1;
+            if (a >> mm & 1) a ^= poly;
+        }
+        return r;
+    };
+    unsigned vec[16] = {}, pre[16] = {};                 // indexed by pivot bit
+    bool have[16] = {};
+    for (unsigned i = 0; i < mm; ++i) {
+        unsigned v = mul(1u << i, 1u << i) ^ (1u << i), p = 1u << i;
+        for (int b = (int)mm - 1; b >= 0; --b)
+            if ((v >> b & 1) && have[b]) { v ^= vec[b]; p ^= pre[b]; }
+        if (!v) continue;
+        const int hb = 31 - __builtin_clz(v);
+        for (int b = 0; b < 16; ++b)                        // keep the basis fully reduced
+            if (have[b] && (vec[b] >> hb & 1)) { vec[b] ^= v; pre[b] ^= p; }
+        vec[hb] = v; pre[hb] = p; have[hb] = true;
+    }
+    for (unsigned j = 0; j < 16; ++j) out[j] = (uint16_t)(j < mm && have[j] ? pre[j] : 0);
+}
+
 bool wide_build_consts(int id, const CodecMath &m, std::vector<uint16_t> &blob) {
     const unsigned NN = m.nn, NR = m.spec.nroots;
     if (NR > wide::kMaxNR) return false;
@@ -732,8 +875,10 @@ hipError_t launch_wide_decode(int id, const DevCodec &d, const DecodeArgs &a, co
     f.queue = w.queue;
     hipLaunchKernelGGL(wide::k_wide_finish<false>, dim3((unsigned)((a.ncw + 7) / 8)), dim3(256), 0, s, f);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    wide::ErrArgs ea{d, a, w.syn, w.queue};
-    const size_t smem = (((size_t)d.nn + wide::kExt + 7) & ~(size_t)7) * 2 + wide::kErrWaves * wide::kErrScratch * 4;
+    wide::ErrArgs ea{d, a, w.syn, w.queue, 0, {}};
+    quad_solver(d.poly, d.mm, ea.qsolve);
+    if (const char *st = getenv("EZRS_WIDE_STOP")) ea.stop = (uint32_t)atoi(st);
+    const size_t smem = (((size_t)d.nn + 7) & ~(size_t)7) * 2 + wide::kErrWaves * wide::kErrScratch * 4;
     const unsigned grid = (unsigned)(d.ncu > 0 ? d.ncu : 256);
     static const hipError_t attr = hipFuncSetAttribute(
         reinterpret_cast<const void *>(&wide::k_wide_errors),
