@@ -32,7 +32,8 @@ constexpr int kBuf = kRows * kRowBytes;     // 32 KiB
 constexpr int kLPW = 2;                     // leaders per wave
 constexpr int kNBuf = 2;                    // window ring: the DMA runs kNBuf - 1 windows ahead
 // (measured alternatives, C4 k_wide_rem per launch: 2 leaders x 8 waves, 2 buffers, 2 workgroups
-// per CU 3.8 ms; 1 leader x 16 waves, 3 buffers, 1 workgroup per CU 4.7 ms)
+// per CU 3.8 ms; 1 leader x 16 waves, 3 buffers, 1 workgroup per CU 4.7 ms; 4 leaders x 4 waves,
+// 2 workgroups per CU 3.8 ms, with half the waves for the 8-leader codec)
 constexpr int kMaxNR = 32;
 constexpr int kM = 16;                      // symbol bits of every wide codec
 constexpr int32_t kSentinel = INT32_MIN;
@@ -62,6 +63,15 @@ struct RemArgs {
     uint16_t *rem;              // [ncw][nlp][16]
     uint32_t nlp;               // leaders padded to the waves (NW * kLPW)
 };
+
+// the networks of leaders B .. B + kLPW - 1 on one 16-symbol block
+template <class C, int B, int L = 0>
+__device__ __forceinline__ void blocks_of(uint32_t (&S)[kLPW][16], const uint32_t (&c)[16]) {
+    if constexpr (L < kLPW && B + L < C::NL) {
+        C::template block<B + L>(S[L], c);
+        blocks_of<C, B, L + 1>(S, c);
+    }
+}
 
 // LDS image of one window: row r (pair p = r >> 1) at r * 256; its 16-byte chunk c = 2b + h
 // (b = 16-symbol block) at slot 2 (b ^ (p & 7)) + (h ^ q), q = (p >> 3) & 1.  Each 16-lane group
@@ -165,8 +175,7 @@ __device__ __forceinline__ void rem_body(const RemArgs &a, uint8_t *lds, int lan
                 c[2 * t] = __builtin_amdgcn_perm(rb[t], ra[t], 0x05040100u);
                 c[2 * t + 1] = __builtin_amdgcn_perm(rb[t], ra[t], 0x07060302u);
             }
-            C::template block<kLPW * W>(S[0], c);
-            if constexpr (kLPW == 2 && kLPW * W + 1 < C::NL) C::template block<kLPW * W + 1>(S[kLPW - 1], c);
+            blocks_of<C, kLPW * W>(S, c);
         }
     }
     // remainders of the lane's two codewords (low halves: row 2p, high halves: row 2p + 1)
@@ -291,7 +300,6 @@ struct ErrArgs {
     DecodeArgs d;
     const uint16_t *syn;
     const uint32_t *queue;
-    uint32_t stop;              // PHASE EXPERIMENT
     uint16_t qsolve[16];        // y = sum_j c_j qsolve[j] solves y^2 + y = c when Tr(c) = 0
 };
 
@@ -424,7 +432,6 @@ __global__ void __launch_bounds__(64 * kErrWaves) k_wide_errors(ErrArgs ea) {
         if (!__ballot(sp != 0)) { if (lane == 0) a.result[k] = 0; continue; }   // 1416-1434
         const unsigned sl = sp ? I[sp] : A0;                 // syn[lane], index form
         slg[lane] = (uint16_t)sl;
-        if (ea.stop == 1) { if (lane == 0) a.result[k] = -1; continue; }
 
         // erasure locator (1436-1450): lane j holds lambda[j] (polynomial form)
         unsigned lam = lane == 0 ? 1u : 0u;
@@ -467,7 +474,6 @@ __global__ void __launch_bounds__(64 * kErrWaves) k_wide_errors(ErrArgs ea) {
         const uint64_t nzl = __ballot(lam != 0 && lane <= NR);
         const unsigned deg = 63 - __builtin_clzll(nzl);
         llg[lane] = (uint16_t)llog;
-        if (ea.stop == 2) { if (lane == 0) a.result[k] = -1; continue; }
         if (deg == 0) {                                      // 1577-1595 (no root can match)
             if (lane == 0) a.result[k] = -1;
             continue;
@@ -482,17 +488,40 @@ __global__ void __launch_bounds__(64 * kErrWaves) k_wide_errors(ErrArgs ea) {
         // r = alpha^i, i in [1, NN] as the reference numbers positions.
         const unsigned Ll = pmonic_log(g, lam, (int)deg);
         const unsigned x1 = deg >= 2 ? (lane == 1 ? 1u : 0u) : (lane == 0 ? pexp(g, Ll) : 0u);
+        // squaring is GF(2)-linear: (sum_j p_j x^j)^2 = sum_j p_j^2 Q_j with Q_j = x^(2j) mod L, so
+        // each squaring is deg independent products per lane once the Q_j are known (x^i mod L
+        // for i <= 2 deg - 2, one multiply-by-x step each)
+        unsigned Ql[kMaxNR];                                 // log form of Q_j
+        {
+            unsigned X = lane == 0 ? 1u : 0u;
+#pragma unroll
+            for (int i = 0; i <= 2 * kMaxNR - 2; ++i) {
+                if (i > 2 * (int)deg - 2) break;
+                if ((i & 1) == 0) Ql[i >> 1] = plog(g, X);
+                const unsigned top = __builtin_amdgcn_readlane(X, deg - 1);
+                X = __shfl_up(X, 1, 64);
+                if (lane == 0 || lane >= deg) X = 0;
+                if (top) {                                   // x^deg = sum_(m < deg) L_m x^m
+                    const unsigned lt = __builtin_amdgcn_readfirstlane(I[top]);
+                    if (lane < deg && Ll != A0) X ^= AT[red1(lt + Ll, NN)];
+                }
+            }
+        }
         unsigned Pl[kM];                                     // log form of P_0 .. P_(m-1)
         unsigned P = x1;
 #pragma unroll
         for (int kk = 0; kk < kM; ++kk) {
             Pl[kk] = plog(g, P);
-            const unsigned src = __shfl(Pl[kk], (int)(lane >> 1), 64);
-            const unsigned sq = (lane & 1) == 0 && src != A0 ? AT[red1(2 * src, NN)] : 0u;
-            P = pmod(g, sq, 2 * (int)deg - 2, Ll, (int)deg, lane);
+            unsigned acc = 0;
+#pragma unroll
+            for (int j = 0; j < kMaxNR; ++j) {
+                if (j >= (int)deg) break;
+                const unsigned lp = __builtin_amdgcn_readlane(Pl[kk], j);
+                if (lp != A0 && Ql[j] != A0) acc ^= AT[red1(red1(2 * lp, NN) + Ql[j], NN)];
+            }
+            P = acc;
         }
         count = __ballot(P != x1) ? -1 : 0;
-        if (ea.stop == 4) { if (lane == 0) a.result[k] = -1; continue; }
         if (count == 0) {
             if (lane <= deg) pool[lane] = (uint16_t)pexp(g, Ll);
             if (lane == 0) stk[0] = deg << 8;                // off | deg << 8 | first b << 16
@@ -574,7 +603,6 @@ __global__ void __launch_bounds__(64 * kErrWaves) k_wide_errors(ErrArgs ea) {
             if (lane == 0) a.result[k] = -1;
             continue;
         }
-        if (ea.stop == 3) { if (lane == 0) a.result[k] = -1; continue; }
         // Omega = S Lambda mod x^NR (1596-1604): lane i <= deg - 1
         const unsigned deg_omega = deg - 1;
         if (lane <= deg_omega) {
@@ -875,9 +903,8 @@ hipError_t launch_wide_decode(int id, const DevCodec &d, const DecodeArgs &a, co
     f.queue = w.queue;
     hipLaunchKernelGGL(wide::k_wide_finish<false>, dim3((unsigned)((a.ncw + 7) / 8)), dim3(256), 0, s, f);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    wide::ErrArgs ea{d, a, w.syn, w.queue, 0, {}};
+    wide::ErrArgs ea{d, a, w.syn, w.queue, {}};
     quad_solver(d.poly, d.mm, ea.qsolve);
-    if (const char *st = getenv("EZRS_WIDE_STOP")) ea.stop = (uint32_t)atoi(st);
     const size_t smem = (((size_t)d.nn + 7) & ~(size_t)7) * 2 + wide::kErrWaves * wide::kErrScratch * 4;
     const unsigned grid = (unsigned)(d.ncu > 0 ? d.ncu : 256);
     static const hipError_t attr = hipFuncSetAttribute(

@@ -156,3 +156,52 @@ def test_wide_corrections_and_bad_erasures(torch, wide):
         if er > 0:
             np.testing.assert_array_equal(got_c[i, :er], cc[:er])
     assert list(r[:4]) == [4, 2, 0, -1] and r[4] == 1
+
+
+def test_wide_root_finder_degrees(torch):
+    """The error path's root finder (Berlekamp trace splitting, direct quadratic solve) at every
+    locator degree 1..32: e errors + f erasures with 2e + f <= 32 in turn, then overwhelmed rows
+    (locators that do not split over GF(2^16), or split with repeated roots), repeated erasure
+    positions, erasures on the parity and on the first and last symbols."""
+    n, k, L = 65535, 65503, 900
+    nr = n - k
+    c = _codec(n, k, True)
+    oc = O.Codec(*O.rs_params(n, k))
+    rng = np.random.default_rng(77)
+    plan = [(e, f) for e in range(17) for f in range(nr - 2 * e + 1)]        # all correctable loads
+    plan += [(e, 0) for e in range(17, 33)] * 6 + [(e, 4) for e in range(15, 30)] * 4
+    ncw = len(plan) + 40
+    ref = rng.integers(0, n + 1, (ncw, L + nr)).astype(np.uint16)
+    oc.encode_batch(ref, L)
+    cw = ref.copy()
+    eras = np.zeros((ncw, nr), np.uint32)
+    neras = np.zeros(ncw, np.uint32)
+    for i, (e, f) in enumerate(plan):
+        locs = rng.choice(L + nr, e + f, replace=False)
+        if i % 3 == 0 and e + f >= 2:
+            locs[0], locs[-1] = 0, L + nr - 1
+        cw[i, locs] ^= rng.integers(1, n + 1, e + f).astype(np.uint16)
+        f = min(f, nr)
+        eras[i, :f] = locs[e:e + f]
+        neras[i] = f
+    for i in range(len(plan), ncw):              # repeated erasure positions, 1-3 errors
+        e = 1 + i % 3
+        locs = rng.choice(L + nr, e + 2, replace=False)
+        cw[i, locs[:e]] ^= 1 + (i % 65535)
+        eras[i, :4] = [locs[e], locs[e + 1], locs[e], L + nr - 1 - i % nr]
+        neras[i] = 4
+    exp = cw.copy()
+    exp_pos = np.zeros((ncw, nr), np.uint32)
+    exp_r = oc.decode_batch(exp, L, None, eras, neras, exp_pos, nthreads=8)
+    d = _dev(torch, cw)
+    pos = torch.zeros((ncw, nr), dtype=torch.int32, device="cuda")
+    r = c.decode(d, L, eras=torch.from_numpy(eras.view(np.int32)).cuda(),
+                 neras=torch.from_numpy(neras.view(np.int32)).cuda(), positions=pos)
+    torch.cuda.synchronize()
+    r = r.cpu().numpy()
+    np.testing.assert_array_equal(r, exp_r)
+    np.testing.assert_array_equal(_host(d), exp)
+    got = pos.cpu().numpy().view(np.uint32)
+    for i in np.nonzero(r > 0)[0]:
+        np.testing.assert_array_equal(got[i, :r[i]], exp_pos[i, :r[i]])
+    assert (r[:len(plan)][:300] > 0).sum() > 250 and (r == -1).sum() > 50
