@@ -16,8 +16,9 @@ Blocks of CB symbols c_0..c_(CB-1) (c_0 first) update the 16 remainder words s[0
 so s'[k] is the XOR of the s[i] with bit k of x^(CB+i) mod M_e set and of the c_t with bit k of
 x^(CB-1-t) mod M_e set.  A cost-driven greedy elimination forms shared pairs and triples once
 (one v_xor / v_bitop3 each), and every row is a chain of three-input XORs.  check_network()
-evaluates each generated network against the bit-serial remainder.  CB = 32 costs about a quarter
-fewer operations per symbol than CB = 16 (more inputs per row to share).
+evaluates each generated network against the bit-serial remainder.  Per 16 symbols and 16 leaders:
+CB = 16 costs 719 ops (828 with the earlier pair-only elimination), CB = 32 615, CB = 64 533 --
+more inputs per row to share; the kernel holds CB inputs plus its leaders' states in VGPRs.
 
 A 32-bit word packs the same position of two codewords (low half: even codeword of the lane's
 pair, high half: odd), so every XOR advances two codewords.
@@ -34,7 +35,7 @@ CODECS = [
     (16, 0x1100B, 1, 1, 32),
     (16, 0x1100B, 1, 1, 16),
 ]
-CB = 32                                       # symbols per network block
+CB = 64                                       # symbols per network block
 
 
 class GF:
@@ -216,7 +217,7 @@ def gen_codec(m, poly, fcr, prim, nr):
         f"C{m}_{poly:x}_{fcr}_{prim}_{nr}"
     out = [f"// ---- {tag}: m={m} poly={poly:#x} fcr={fcr} prim={prim} nroots={nr}: "
            f"{len(lead)} coset leaders ----"]
-    # slot order: waves take slots (2w, 2w+1); pair the costliest networks with the cheapest so
+    # slot order: waves take consecutive slots (kLPW per wave); alternate the costliest networks with the cheapest so
     # that the waves of a workgroup reach each window's barrier together
     cost = {}
     for e in lead:

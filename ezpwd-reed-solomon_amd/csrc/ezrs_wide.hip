@@ -29,11 +29,12 @@ constexpr int kRows = 128;                  // codewords per tile (64 pairs)
 constexpr int kWin = 128;                   // symbols per window
 constexpr int kRowBytes = 2 * kWin;         // 256 B of each row per window
 constexpr int kBuf = kRows * kRowBytes;     // 32 KiB
-constexpr int kLPW = 2;                     // leaders per wave
+constexpr int kLPW = 4;                     // leaders per wave
 constexpr int kNBuf = 2;                    // window ring: the DMA runs kNBuf - 1 windows ahead
-// (measured alternatives, C4 k_wide_rem per launch: 2 leaders x 8 waves, 2 buffers, 2 workgroups
-// per CU 3.8 ms; 1 leader x 16 waves, 3 buffers, 1 workgroup per CU 4.7 ms; 4 leaders x 4 waves,
-// 2 workgroups per CU 3.8 ms, with half the waves for the 8-leader codec)
+// (measured, C4 k_wide_rem per launch.  16-symbol networks: 2 leaders x 8 waves, 2 workgroups per
+// CU 3.8 ms; 1 leader x 16 waves, 3 buffers, 1 workgroup per CU 4.7 ms; 4 leaders x 4 waves
+// 3.8 ms.  32-symbol networks, 2 leaders x 8 waves: 3.27 ms.  64-symbol networks (C::CB), 4 leaders
+// x 4 waves, 198 VGPRs, 2 workgroups per CU: 2.89 ms.)
 constexpr int kMaxNR = 32;
 constexpr int kM = 16;                      // symbol bits of every wide codec
 constexpr int32_t kSentinel = INT32_MIN;
