@@ -34,8 +34,8 @@ struct ezrs_codec {
     int bs_id = -1;               // bit-sliced GF(2^8) kernel set, -1 if none
     int ps_id = -1;               // plane-sliced GF(2^8) kernel set, -1 if none
     int wide_id = -1;             // GF(2^16) remainder kernel set, -1 if none
-    std::vector<uint16_t> wide_blob;   // host: leader slots | log beta | log Q
-    uint16_t *d_qlog = nullptr;   // device copy of log Q
+    std::vector<uint16_t> wide_blob;   // host: leader slots | log beta | column tables
+    uint16_t *d_wcols = nullptr;  // device copy of the column tables (constant multipliers)
     // Device workspaces of the batch entry points, one per HIP stream: calls on different streams
     // never share scratch memory, calls on one stream are ordered by the stream.  A workspace only
     // grows; the buffer it replaces is kept until ezrs_destroy, so work already queued (or a
@@ -169,9 +169,9 @@ int ezrs_create(ezrs_codec **out, unsigned symbol_bits, unsigned poly, unsigned 
         if (!wide_build_consts(c->wide_id, m, c->wide_blob)) {
             c->wide_id = -1;
         } else {
-            const size_t qn = (size_t)m.spec.nroots * m.spec.nroots;
-            if ((e = hipMalloc(&c->d_qlog, qn * sizeof(uint16_t))) != hipSuccess ||
-                (e = hipMemcpy(c->d_qlog, c->wide_blob.data() + 64, qn * sizeof(uint16_t),
+            const size_t qn = wide_cols_count(m.spec.nroots);
+            if ((e = hipMalloc(&c->d_wcols, qn * sizeof(uint16_t))) != hipSuccess ||
+                (e = hipMemcpy(c->d_wcols, c->wide_blob.data() + 64, qn * sizeof(uint16_t),
                                hipMemcpyHostToDevice)) != hipSuccess) {
                 ezrs_destroy(c);
                 return hip_fail(e, "hipMalloc(wide tables)");
@@ -207,7 +207,7 @@ int ezrs_destroy(ezrs_codec *c) {
     DeviceGuard g(c->device);
     (void)hipFree(c->d_tabs);
     (void)hipFree(c->d_dual);
-    if (c->d_qlog) (void)hipFree(c->d_qlog);
+    if (c->d_wcols) (void)hipFree(c->d_wcols);
     for (auto &kv : c->ws) (void)hipFree(kv.second.p);
     for (void *p : c->ws_retired) (void)hipFree(p);
     for (int i = 0; i < 2; ++i) {
@@ -273,7 +273,7 @@ namespace {
 hipError_t dispatch_encode(const ezrs_codec *c, const EncodeArgs &a, void *ws, hipStream_t st) {
     if (c->ps_id >= 0 && ps_can_encode(c->dev, a)) return launch_ps_encode(c->ps_id, c->dev, a, ws, st);
     if (c->wide_id >= 0 && wide_can_encode(c->dev, a))
-        return launch_wide_encode(c->wide_id, c->dev, a, c->wide_blob.data(), c->d_qlog, ws, st);
+        return launch_wide_encode(c->wide_id, c->dev, a, c->wide_blob.data(), c->d_wcols, ws, st);
     return c->bs_id >= 0 ? launch_bs_encode(c->bs_id, c->dev, a, ws, st) : launch_encode_generic(c->dev, a, st);
 }
 
@@ -289,7 +289,7 @@ hipError_t dispatch_decode(const ezrs_codec *c, const DecodeArgs &a, uint8_t *sy
         return e;
     }
     if (c->wide_id >= 0 && wide_can_decode(c->dev, a))
-        return launch_wide_decode(c->wide_id, c->dev, a, c->wide_blob.data(), c->d_qlog, syn_ws, st);
+        return launch_wide_decode(c->wide_id, c->dev, a, c->wide_blob.data(), c->d_wcols, syn_ws, st);
     if (c->bs_id >= 0 && contiguous) {
         // Bit-sliced syndromes for the whole batch; the reference algorithm only for the codewords
         // that are not valid as received (or carry erasures to validate).

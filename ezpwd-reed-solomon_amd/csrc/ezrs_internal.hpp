@@ -95,11 +95,12 @@ size_t wide_ws_bytes(int id, size_t ncw);
 // blob: syndrome leader slots [32] | log beta [32] | log Q [NR][NR] (host copy; the Q part is
 // also uploaded to the device)
 bool wide_build_consts(int id, const CodecMath &m, std::vector<uint16_t> &blob);
+size_t wide_cols_count(unsigned nroots);   // u16 entries of the device column tables (blob + 64)
 bool wide_can_encode(const DevCodec &d, const EncodeArgs &a);
 bool wide_can_decode(const DevCodec &d, const DecodeArgs &a);
 hipError_t launch_wide_encode(int id, const DevCodec &d, const EncodeArgs &a, const uint16_t *blob_host,
-                              const uint16_t *qlog_dev, void *ws, hipStream_t s);
+                              const uint16_t *cols_dev, void *ws, hipStream_t s);
 hipError_t launch_wide_decode(int id, const DevCodec &d, const DecodeArgs &a, const uint16_t *blob_host,
-                              const uint16_t *qlog_dev, void *ws, hipStream_t s);
+                              const uint16_t *cols_dev, void *ws, hipStream_t s);
 
 } // namespace ezrs

@@ -223,12 +223,10 @@ __global__ void __launch_bounds__(64 * ((C::NL + kLPW - 1) / kLPW)) k_wide_rem(R
 // ------------------------------------------------------------------------------------------------
 struct FinishArgs {
     const uint16_t *rem;
-    uint32_t nlp, ncw, nr, nn;
-    const uint16_t *alpha_to, *index_of;
+    uint32_t nlp, ncw, nr;
     uint8_t leader[kMaxNR];     // syndrome i -> leader slot
-    uint16_t elog[kMaxNR];      // log beta_i = (fcr + i) prim mod NN
+    const uint16_t *cols;       // [NR][16] beta_i * 2^b, then (encode) [NR][NR][16] Q_ki * 2^b
     // encode
-    const uint16_t *qlog;       // [NR][NR] log Q (NN for 0)
     uint16_t *parity;
     size_t pstride;             // elements
     // decode
@@ -238,64 +236,97 @@ struct FinishArgs {
     uint32_t *queue;            // [0] count, [1..] flagged codewords
 };
 
+constexpr int kFinGroups = 8;               // codewords per block pass (32 lanes each)
+constexpr int kQRow = 2 * kMaxNR * 16 + 16; // bytes per LDS row of Q columns (padded)
+
+// x * c for a constant c given by its columns col[b] = c * 2^b: XOR of the columns of x's set bits
+// (v_bfe_i32 gives the all-ones / zero mask, v_bitop3 0x78 is y ^ (col & mask)); no table reads
+__device__ __forceinline__ uint32_t mulc(uint32_t x, const uint32_t (&col)[16]) {
+    uint32_t y = 0;
+#pragma unroll
+    for (int b = 0; b < 16; ++b)
+        y = __builtin_amdgcn_bitop3_b32(y, col[b], (uint32_t)__builtin_amdgcn_sbfe((int)x, b, 1), 0x78);
+    return y;
+}
+
 template <bool ENC>
 __global__ void __launch_bounds__(256) k_wide_finish(FinishArgs a) {
-    __shared__ uint16_t sl[8][kMaxNR];
+    __shared__ uint16_t sl[kFinGroups][kMaxNR];
+    __shared__ __attribute__((aligned(16))) uint8_t qc[ENC ? kMaxNR * kQRow : 16];
+    __shared__ uint32_t nfl[kFinGroups], qbase;
     const unsigned lane = threadIdx.x & 31, g = threadIdx.x >> 5;
-    const size_t cw = (size_t)blockIdx.x * 8 + g;
-    const bool live = cw < a.ncw;
-    const unsigned NN = a.nn;
-    uint32_t S = 0;
-    if (live && lane < a.nr) {
-        const uint4 *src = reinterpret_cast<const uint4 *>(a.rem + (cw * a.nlp + a.leader[lane]) * 16);
-        const uint4 r0 = src[0], r1 = src[1];
-        const uint32_t rw[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
-        const unsigned e = a.elog[lane];
-        unsigned ek = 0;                                   // e * k mod NN
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const unsigned r = (rw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
-            if (r) {
-                unsigned x = a.index_of[r] + ek;
-                x = x >= NN ? x - NN : x;
-                S ^= a.alpha_to[x];
-            }
-            ek += e;
-            ek = ek >= NN ? ek - NN : ek;
+    const unsigned NR = a.nr;
+    if constexpr (ENC) {                      // Q columns: row k = the 16 NR columns of parity k
+        const unsigned rowb = NR * 32;
+        for (unsigned t = threadIdx.x; t < NR * rowb / 16; t += 256) {
+            const unsigned k = t / (rowb / 16), o = t % (rowb / 16);
+            *reinterpret_cast<uint4 *>(qc + k * kQRow + 16 * o) =
+                reinterpret_cast<const uint4 *>(a.cols + NR * 16 + k * NR * 16)[o];
         }
     }
-    if constexpr (ENC) {
-        sl[g][lane] = (uint16_t)(S ? a.index_of[S] : NN);
-        __syncthreads();
-        if (!live || lane >= a.nr) return;
-        const uint16_t *qrow = a.qlog + lane * a.nr;
-        uint32_t par = 0;
-        for (unsigned i = 0; i < a.nr; ++i) {
-            const unsigned s = sl[g][i], qv = qrow[i];
-            if (s != NN && qv != NN) {
-                unsigned x = s + qv;
-                x = x >= NN ? x - NN : x;
-                par ^= a.alpha_to[x];
+    uint32_t bc[16];                          // columns of beta_lane
+    if (lane < NR) {
+        const uint4 *cp = reinterpret_cast<const uint4 *>(a.cols + lane * 16);
+        const uint4 c0 = cp[0], c1 = cp[1];
+        const uint32_t w[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+        for (int b = 0; b < 16; ++b) bc[b] = (w[b >> 1] >> (16 * (b & 1))) & 0xFFFFu;
+    }
+    for (size_t base = (size_t)blockIdx.x * kFinGroups; base < a.ncw; base += (size_t)gridDim.x * kFinGroups) {
+        const size_t cw = base + g;
+        const bool live = cw < a.ncw;
+        uint32_t S = 0;                       // S_lane = R(beta) by Horner, R = sum_k s[k] x^k
+        if (live && lane < NR) {
+            const uint4 *src = reinterpret_cast<const uint4 *>(a.rem + (cw * a.nlp + a.leader[lane]) * 16);
+            const uint4 r0 = src[0], r1 = src[1];
+            const uint32_t rw[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+#pragma unroll
+            for (int k = 15; k >= 0; --k) S = mulc(S, bc) ^ ((rw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
+        }
+        if constexpr (ENC) {
+            __syncthreads();                  // Q staged (first pass); sl free (later passes)
+            sl[g][lane] = (uint16_t)S;
+            __syncthreads();
+            if (live && lane < NR) {
+                const uint8_t *qrow = qc + lane * kQRow;
+                uint32_t par = 0;
+                for (unsigned i = 0; i < NR; ++i) {
+                    const uint4 q0 = *reinterpret_cast<const uint4 *>(qrow + 32 * i);
+                    const uint4 q1 = *reinterpret_cast<const uint4 *>(qrow + 32 * i + 16);
+                    const uint32_t w[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+                    uint32_t qcol[16];
+#pragma unroll
+                    for (int b = 0; b < 16; ++b) qcol[b] = (w[b >> 1] >> (16 * (b & 1))) & 0xFFFFu;
+                    par ^= mulc(sl[g][i], qcol);
+                }
+                a.parity[cw * a.pstride + lane] = (uint16_t)par;
             }
+        } else {
+            // flagged codewords (nonzero syndromes or erasures) go to the error queue, one
+            // atomic per block pass (a counter hit once per codeword serialises)
+            const uint64_t nz = __ballot(S != 0);
+            const uint32_t half = (uint32_t)(nz >> (32 * (g & 1)));
+            const bool flagged = live && (half != 0 || (a.neras && a.neras[cw] != 0));
+            if (flagged && lane < NR) a.syn[cw * kMaxNR + lane] = (uint16_t)S;   // zeros too
+            if (lane == 0) {
+                nfl[g] = flagged ? 1u : 0u;
+                if (live) a.result[cw] = flagged ? kSentinel : 0;
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                unsigned n = 0;
+#pragma unroll
+                for (int j = 0; j < kFinGroups; ++j) n += nfl[j];
+                qbase = n ? atomicAdd(a.queue, n) : 0u;
+            }
+            __syncthreads();
+            if (lane == 0 && flagged) {
+                unsigned below = 0;
+                for (unsigned j = 0; j < g; ++j) below += nfl[j];
+                a.queue[1 + qbase + below] = (uint32_t)cw;
+            }
+            __syncthreads();                  // nfl / qbase reused by the next pass
         }
-        a.parity[cw * a.pstride + lane] = (uint16_t)par;
-    } else {
-        const uint64_t nz = __ballot(S != 0);
-        const uint32_t half = (uint32_t)(nz >> (32 * (g & 1)));
-        if (!live || lane != 0) {
-            if (live && half && lane < a.nr) a.syn[cw * kMaxNR + lane] = (uint16_t)S;
-            return;
-        }
-        const bool flagged = half != 0 || (a.neras && a.neras[cw] != 0);
-        if (flagged && lane < a.nr) a.syn[cw * kMaxNR] = (uint16_t)S;
-        if (flagged) {
-            // syndromes of a codeword with erasures but zero syndromes are zero: write them all
-            if (!half)
-                for (unsigned i = 0; i < a.nr; ++i) a.syn[cw * kMaxNR + i] = 0;
-            const uint32_t at = atomicAdd(a.queue, 1u);
-            a.queue[1 + at] = (uint32_t)cw;
-        }
-        a.result[cw] = flagged ? kSentinel : 0;
     }
 }
 
@@ -707,14 +738,6 @@ hipError_t launch_rem(const uint8_t *base, size_t stride_bytes, uint32_t n, size
 
 } // namespace
 
-// Per-codec constants of the finishing kernel (syndrome -> leader slot, log beta, log Q).
-struct WideConsts {
-    uint8_t leader[wide::kMaxNR];
-    uint16_t elog[wide::kMaxNR];
-    std::vector<uint16_t> qlog;   // [NR][NR]
-    uint32_t nlp;
-};
-
 int wide_codec_id(const DevCodec &d) {
     int id = 0, found = -1;
 #define EZRS_WIDE_MATCH(C) \
@@ -824,37 +847,42 @@ bool wide_build_consts(int id, const CodecMath &m, std::vector<uint16_t> &blob) 
             }
         }
     }
-    // blob: leader[32] (as u16) | elog[32] | qlog[NR*NR]
-    blob.assign(2 * wide::kMaxNR + NR * NR, 0);
+    // blob: leader[32] (as u16) | elog[32] | columns (the device copy): beta_i * 2^b [NR][16], then
+    // Q_ki * 2^b [NR][NR][16] with Q = V^-1 diag(beta^NR): parity_k = sum_i Q_ki S_i
+    blob.assign(2 * wide::kMaxNR + NR * 16 + NR * NR * 16, 0);
     for (unsigned i = 0; i < NR; ++i) {
         blob[i] = li[i];
         blob[wide::kMaxNR + i] = el[i];
+        const unsigned beta = gf.pow_alpha(el[i]);
+        for (unsigned b = 0; b < 16; ++b) blob[2 * wide::kMaxNR + i * 16 + b] = (uint16_t)gf.mul(beta, 1u << b);
     }
+    uint16_t *qc = blob.data() + 2 * wide::kMaxNR + NR * 16;
     for (unsigned k = 0; k < NR; ++k)
         for (unsigned i = 0; i < NR; ++i) {
             const unsigned bn = gf.pow_alpha((unsigned)(((uint64_t)el[i] * NR) % NN));
             const unsigned q = gf.mul(Inv[k * NR + i], bn);
-            blob[2 * wide::kMaxNR + k * NR + i] = (uint16_t)(q ? gf.index_of[q] : NN);
+            for (unsigned b = 0; b < 16; ++b) qc[(k * NR + i) * 16 + b] = (uint16_t)gf.mul(q, 1u << b);
         }
     return true;
 }
 
+size_t wide_cols_count(unsigned nroots) { return (size_t)nroots * 16 + (size_t)nroots * nroots * 16; }
+
 static wide::FinishArgs finish_args(const DevCodec &d, int id, const uint16_t *blob_host,
-                                    const uint16_t *qlog_dev, size_t ncw, uint16_t *rem) {
+                                    const uint16_t *cols_dev, size_t ncw, uint16_t *rem) {
     wide::FinishArgs f{};
     f.rem = rem;
     f.nlp = wide_nlp(id);
     f.ncw = (uint32_t)ncw;
     f.nr = d.nroots;
-    f.nn = d.nn;
-    f.alpha_to = d.alpha_to;
-    f.index_of = d.index_of;
-    for (unsigned i = 0; i < d.nroots; ++i) {
-        f.leader[i] = (uint8_t)blob_host[i];
-        f.elog[i] = blob_host[wide::kMaxNR + i];
-    }
-    f.qlog = qlog_dev;
+    for (unsigned i = 0; i < d.nroots; ++i) f.leader[i] = (uint8_t)blob_host[i];
+    f.cols = cols_dev;
     return f;
+}
+
+static unsigned finish_grid(const DevCodec &d, size_t ncw) {
+    const size_t want = (ncw + wide::kFinGroups - 1) / wide::kFinGroups, cap = (size_t)(d.ncu > 0 ? d.ncu : 256) * 8;
+    return (unsigned)(want < cap ? want : cap);
 }
 
 bool wide_can_encode(const DevCodec &, const EncodeArgs &a) {
@@ -870,7 +898,7 @@ bool wide_can_decode(const DevCodec &d, const DecodeArgs &a) {
 }
 
 hipError_t launch_wide_encode(int id, const DevCodec &d, const EncodeArgs &a, const uint16_t *blob_host,
-                              const uint16_t *qlog_dev, void *ws, hipStream_t s) {
+                              const uint16_t *cols_dev, void *ws, hipStream_t s) {
     if (a.ncw == 0) return hipSuccess;
     WideWs w = carve(ws, a.ncw);
     const size_t sb = 2 * (a.ncw > 1 ? a.data_stride : (size_t)a.len);
@@ -881,15 +909,15 @@ hipError_t launch_wide_encode(int id, const DevCodec &d, const EncodeArgs &a, co
     EZRS_WIDE_CODEC_LIST(EZRS_WIDE_ENC)
 #undef EZRS_WIDE_ENC
     if (e != hipSuccess) return e;
-    wide::FinishArgs f = finish_args(d, id, blob_host, qlog_dev, a.ncw, w.rem);
+    wide::FinishArgs f = finish_args(d, id, blob_host, cols_dev, a.ncw, w.rem);
     f.parity = static_cast<uint16_t *>(a.parity);
     f.pstride = a.parity_stride;
-    hipLaunchKernelGGL(wide::k_wide_finish<true>, dim3((unsigned)((a.ncw + 7) / 8)), dim3(256), 0, s, f);
+    hipLaunchKernelGGL(wide::k_wide_finish<true>, dim3(finish_grid(d, a.ncw)), dim3(256), 0, s, f);
     return hipGetLastError();
 }
 
 hipError_t launch_wide_decode(int id, const DevCodec &d, const DecodeArgs &a, const uint16_t *blob_host,
-                              const uint16_t *qlog_dev, void *ws, hipStream_t s) {
+                              const uint16_t *cols_dev, void *ws, hipStream_t s) {
     if (a.ncw == 0) return hipSuccess;
     WideWs w = carve(ws, a.ncw);
     hipError_t e = hipMemsetAsync(w.queue, 0, 4, s);
@@ -901,12 +929,12 @@ hipError_t launch_wide_decode(int id, const DevCodec &d, const DecodeArgs &a, co
     EZRS_WIDE_CODEC_LIST(EZRS_WIDE_DEC)
 #undef EZRS_WIDE_DEC
     if (e != hipSuccess) return e;
-    wide::FinishArgs f = finish_args(d, id, blob_host, qlog_dev, a.ncw, w.rem);
+    wide::FinishArgs f = finish_args(d, id, blob_host, cols_dev, a.ncw, w.rem);
     f.neras = a.neras;
     f.result = a.result;
     f.syn = w.syn;
     f.queue = w.queue;
-    hipLaunchKernelGGL(wide::k_wide_finish<false>, dim3((unsigned)((a.ncw + 7) / 8)), dim3(256), 0, s, f);
+    hipLaunchKernelGGL(wide::k_wide_finish<false>, dim3(finish_grid(d, a.ncw)), dim3(256), 0, s, f);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     wide::ErrArgs ea{d, a, w.syn, w.queue, {}};
     quad_solver(d.poly, d.mm, ea.qsolve);
