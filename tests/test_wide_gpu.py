@@ -205,3 +205,33 @@ def test_wide_root_finder_degrees(torch):
     for i in np.nonzero(r > 0)[0]:
         np.testing.assert_array_equal(got[i, :r[i]], exp_pos[i, :r[i]])
     assert (r[:len(plan)][:300] > 0).sum() > 250 and (r == -1).sum() > 50
+
+
+def test_wide_multi_pass_batch(torch):
+    """A batch larger than one pass of the persistent finishing grid (CUs x 64 codewords) and of the
+    error kernel's grid: parity against the oracle, then a decode round trip with 0..16 errors per
+    codeword (result = error count, rows restored)."""
+    n, k, L = 65535, 65503, 97
+    nr = n - k
+    ncw = 40000
+    c = _codec(n, k, True)
+    oc = O.Codec(*O.rs_params(n, k))
+    rng = np.random.default_rng(11)
+    ref = rng.integers(0, n + 1, (ncw, L + nr)).astype(np.uint16)
+    oc.encode_batch(ref, L)
+    h = ref.copy()
+    h[:, L:] = 0
+    dev = _dev(torch, h)
+    c.encode(dev, L)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_host(dev), ref)
+    cw = ref.copy()
+    nerr = np.arange(ncw) % 17
+    for i in range(ncw):
+        locs = rng.choice(L + nr, nerr[i], replace=False)
+        cw[i, locs] ^= rng.integers(1, n + 1, nerr[i]).astype(np.uint16)
+    d = _dev(torch, cw)
+    r = c.decode(d, L)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(r.cpu().numpy(), nerr)
+    np.testing.assert_array_equal(_host(d), ref)
