@@ -6,9 +6,11 @@
 // root beta of the coset gives S = R_e(beta), 16 GF(2^16) products per syndrome.
 //
 //   k_wide_rem     streams 128-codeword tiles through LDS (LDS-DMA, 128-symbol windows, double
-//                  buffered); wave w runs the networks of leaders 2w, 2w+1 on 32-bit words that pack
-//                  one position of two codewords.  Out: remainders [ncw][NLP][16] u16.
-//   k_wide_finish  32 lanes per codeword evaluate the syndromes.  Encode: parity = Q S with
+//                  buffered); wave w runs the 64-symbol networks of leaders kLPW w .. kLPW w + 3 on
+//                  32-bit words that pack one position of two codewords.  Out: remainders
+//                  [ncw][NLP][16] u16.
+//   k_wide_finish  32 lanes per codeword evaluate the syndromes by Horner with a table-free
+//                  multiply by the constant beta (mulc).  Encode: parity = Q S with
 //                  Q = V^-1 diag(beta^NR) (V[i][k] = beta_i^(NR-1-k)), the unique parity whose
 //                  codeword has zero syndromes -- encode_symbols' LFSR result (rs_base:1296-1332).
 //                  Decode: result 0 for a codeword with zero syndromes and no erasures
