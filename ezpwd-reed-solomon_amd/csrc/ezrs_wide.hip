@@ -162,18 +162,41 @@ __device__ __forceinline__ void rem_body(const RemArgs &a, uint8_t *lds, int lan
 #pragma unroll
         for (int b0 = 0; b0 < kWin / 16; b0 += C::CB / 16) {
             uint32_t c[C::CB];
+            static_assert(C::CB == 64, "the LDS read below covers four 16-symbol blocks");
+            uint32_t xa[4], xb[4];
 #pragma unroll
-            for (int h2 = 0; h2 < C::CB / 16; ++h2) {
+            for (int h2 = 0; h2 < 4; ++h2) {
                 const uint32_t blk = wb + 32 * ((uint32_t)(b0 + h2) ^ (p & 7));
-                const uint32_t x0 = blk + 16 * q, x1 = blk + 16 * (q ^ 1);
-                uint4 A0, A1, B0, B1;
-                asm volatile("ds_read_b128 %0, %4\n\t"
-                             "ds_read_b128 %1, %5\n\t"
-                             "ds_read_b128 %2, %4 offset:256\n\t"
-                             "ds_read_b128 %3, %5 offset:256\n\t"
-                             "s_waitcnt lgkmcnt(0)"
-                             : "=&v"(A0), "=&v"(A1), "=&v"(B0), "=&v"(B1)
-                             : "v"(x0), "v"(x1) : "memory");
+                xa[h2] = blk + 16 * q;
+                xb[h2] = blk + 16 * (q ^ 1);
+            }
+            uint4 R[16];                              // [h2][A0, A1, B0, B1]: one wait for all
+            asm volatile("ds_read_b128 %0, %16\n\t"
+                         "ds_read_b128 %1, %17\n\t"
+                         "ds_read_b128 %2, %16 offset:256\n\t"
+                         "ds_read_b128 %3, %17 offset:256\n\t"
+                         "ds_read_b128 %4, %18\n\t"
+                         "ds_read_b128 %5, %19\n\t"
+                         "ds_read_b128 %6, %18 offset:256\n\t"
+                         "ds_read_b128 %7, %19 offset:256\n\t"
+                         "ds_read_b128 %8, %20\n\t"
+                         "ds_read_b128 %9, %21\n\t"
+                         "ds_read_b128 %10, %20 offset:256\n\t"
+                         "ds_read_b128 %11, %21 offset:256\n\t"
+                         "ds_read_b128 %12, %22\n\t"
+                         "ds_read_b128 %13, %23\n\t"
+                         "ds_read_b128 %14, %22 offset:256\n\t"
+                         "ds_read_b128 %15, %23 offset:256\n\t"
+                         "s_waitcnt lgkmcnt(0)"
+                         : "=&v"(R[0]), "=&v"(R[1]), "=&v"(R[2]), "=&v"(R[3]), "=&v"(R[4]), "=&v"(R[5]),
+                           "=&v"(R[6]), "=&v"(R[7]), "=&v"(R[8]), "=&v"(R[9]), "=&v"(R[10]), "=&v"(R[11]),
+                           "=&v"(R[12]), "=&v"(R[13]), "=&v"(R[14]), "=&v"(R[15])
+                         : "v"(xa[0]), "v"(xb[0]), "v"(xa[1]), "v"(xb[1]), "v"(xa[2]), "v"(xb[2]),
+                           "v"(xa[3]), "v"(xb[3])
+                         : "memory");
+#pragma unroll
+            for (int h2 = 0; h2 < 4; ++h2) {
+                const uint4 A0 = R[4 * h2], A1 = R[4 * h2 + 1], B0 = R[4 * h2 + 2], B1 = R[4 * h2 + 3];
                 const uint32_t ra[8] = {A0.x, A0.y, A0.z, A0.w, A1.x, A1.y, A1.z, A1.w};
                 const uint32_t rb[8] = {B0.x, B0.y, B0.z, B0.w, B1.x, B1.y, B1.z, B1.w};
 #pragma unroll
