@@ -507,10 +507,12 @@ __global__ void __launch_bounds__(64 * kErrWaves) k_wide_errors(ErrArgs ea) {
             }
         }
         unsigned b = lam ? I[lam] : A0;                      // b[lane], index form
-        // Berlekamp-Massey (1501-1546); lanes > NR hold lambda = 0, b = A0
+        unsigned li = b;                                     // lambda[lane], index form
+        // Berlekamp-Massey (1501-1546); lanes > NR hold lambda = 0, b = A0.  A step with a zero
+        // discrepancy leaves lambda (and so li) as it is: the log-table read is redone only after
+        // lambda changes.
         unsigned r = no_eras, el = no_eras;
         while (++r <= NR) {
-            const unsigned li = lam ? I[lam] : A0;
             const unsigned si = lane < r ? slg[r - 1 - lane] : A0;
             const unsigned term = (li != A0 && si != A0) ? AT[red1(li + si, NN)] : 0u;
             const unsigned dsum = wave_xor(term);
@@ -528,10 +530,11 @@ __global__ void __launch_bounds__(64 * kErrWaves) k_wide_errors(ErrArgs ea) {
                     b = lane <= NR ? bsh : A0;
                 }
                 lam = lane <= NR ? t : 0u;
+                li = lam ? I[lam] : A0;
             }
         }
         // lambda to index form, its degree (1549-1553)
-        const unsigned llog = lam ? I[lam] : A0;
+        const unsigned llog = li;
         const uint64_t nzl = __ballot(lam != 0 && lane <= NR);
         const unsigned deg = 63 - __builtin_clzll(nzl);
         llg[lane] = (uint16_t)llog;
