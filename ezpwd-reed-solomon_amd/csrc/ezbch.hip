@@ -36,8 +36,8 @@
 
 namespace {
 
-constexpr int kMaxT = 16;
-constexpr int kMaxNW = 4;                    // 64-bit words of the widest remainder
+constexpr int kBigT = 64;                    // runtime-t decode (k_bch_decode_big<NW>)
+constexpr int kMaxNW = 16;                   // 64-bit words of the widest remainder
 constexpr int kMaxM = 15;
 constexpr int kThreads = 256;
 constexpr int kEBADMSG = 74, kEINVAL = 22;   // Linux errno values, negated as decode_bch returns them
@@ -184,7 +184,9 @@ __global__ void __launch_bounds__(kThreads) k_bch_encode(DevBch b, BchArgs a) {
     if (k >= a.ncw) return;
     const Rem<NW> r = data_remainder<NW>(reinterpret_cast<const uint64_t *>(smem), row, a.len);
     uint8_t *e = a.ecc + k * a.estride;
-    for (int i = 0; i < b.ecc_bytes; ++i) e[i] = (uint8_t)(r.w[i >> 3] >> (56 - 8 * (i & 7)));
+    // ecc_bytes = ceil(m t / 8) may pass the NW words when ecc_bits < m t: those bytes are zero
+    for (int i = 0; i < b.ecc_bytes; ++i)
+        e[i] = (i >> 3) < NW ? (uint8_t)(r.w[(i >> 3) < NW ? i >> 3 : 0] >> (56 - 8 * (i & 7))) : (uint8_t)0;
 }
 
 // y -> A4 y^4 + A2 y^2 + A1 y is GF(2)-linear.  With the images of the polynomial-basis vectors
@@ -449,7 +451,8 @@ __global__ void __launch_bounds__(kThreads) k_bch_decode(DevBch b, BchArgs a) {
     } else {
         r = data_remainder<NW>(reinterpret_cast<const uint64_t *>(smem), row, a.len);
     }
-    for (int i = 0; i < b.ecc_bytes; ++i) r.w[i >> 3] ^= (uint64_t)e[i] << (56 - 8 * (i & 7));
+    for (int i = 0; i < b.ecc_bytes && (i >> 3) < NW; ++i)    // bytes past NW words: unused bits
+        r.w[i >> 3] ^= (uint64_t)e[i] << (56 - 8 * (i & 7));
     uint64_t any = 0;
 #pragma unroll
     for (int i = 0; i < NW; ++i) any |= r.w[i];
@@ -476,13 +479,171 @@ __global__ void __launch_bounds__(kThreads) k_bch_decode(DevBch b, BchArgs a) {
     }
 }
 
+// ---- t > 16 or ecc_bits > 256: the same decode with run-time t ------------------------------
+// The working polynomials are per-lane arrays indexed at run time (scratch memory): slower than
+// the register-resident k_bch_decode<T, NW>, for the codecs it does not instantiate.
+
+// Chien search over p < nbits, run-time degree L (as chien<T>)
+__device__ int chien_big(const GF &f, const uint32_t *C, int L, uint32_t nbits, uint32_t *P, int T) {
+    int lt[kBigT + 1];
+    for (int j = 0; j <= L; ++j) lt[j] = C[j] ? (int)f.lg[C[j]] : -1;
+    int cnt = 0;
+    for (uint32_t p = 0; p < nbits; ++p) {
+        uint32_t v = 0;
+        for (int j = 0; j <= L; ++j)
+            if (lt[j] >= 0) {
+                v ^= f.ex[lt[j]];
+                lt[j] += L - j;
+                if (lt[j] >= f.n) lt[j] -= f.n;
+            }
+        if (!v) {
+            if (cnt < T) P[cnt] = p;
+            ++cnt;
+        }
+    }
+    return cnt;
+}
+
+// locate<T, NW> with run-time t <= kBigT
+template <int NW>
+__device__ int locate_big(const DevBch &b, const GF &f, Rem<NW> r, uint32_t nbits, uint32_t *loc) {
+    uint64_t any = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) any |= r.w[i];
+    if (!any) return 0;
+    const int T = b.t;
+    const uint32_t n = (uint32_t)b.n;
+    uint32_t S[2 * kBigT + 1];
+    for (int j = 0; j <= 2 * T; ++j) S[j] = 0;
+#pragma unroll
+    for (int wi = 0; wi < NW; ++wi) {
+        uint64_t x = r.w[wi];
+        while (x) {                         // S_j = r(alpha^j), j odd
+            const int lz = __clzll(x);
+            x &= ~(0x8000000000000000ull >> lz);
+            const uint32_t p = (uint32_t)(b.ecc_bits - 1 - (64 * wi + lz));
+            uint32_t p2 = 2 * p;
+            if (p2 >= n) p2 -= n;
+            uint32_t e = p;
+            for (int j = 1; j < 2 * T; j += 2) {
+                S[j] ^= f.ex[e];
+                e += p2;
+                if (e >= n) e -= n;
+            }
+        }
+    }
+    for (int j = 1; j <= T; ++j) S[2 * j] = f.sq(S[j]);
+    // Berlekamp-Massey as in locate<T, NW>
+    const int W = 2 * T + 2;
+    uint32_t C[2 * kBigT + 2], B[2 * kBigT + 2], old[2 * kBigT + 2];
+    for (int j = 0; j < W; ++j) {
+        C[j] = j == 0;
+        B[j] = j == 1;
+    }
+    int L = 0;
+    uint32_t bd = 1;
+    for (int rr = 1; rr < 2 * T; rr += 2) {
+        uint32_t d = S[rr];
+        for (int i = 1; i < rr; ++i) d ^= f.mul(C[i], S[rr - i]);
+        if (d) {
+            const bool grow = 2 * L <= rr - 1;
+            const uint32_t q = f.div(d, bd);
+            for (int j = 0; j < W; ++j) {
+                old[j] = C[j];
+                C[j] ^= f.mul(q, B[j]);
+            }
+            if (grow) {
+                L = rr - L;
+                bd = d;
+            }
+            for (int j = W - 1; j >= 0; --j) B[j] = j >= 2 ? (grow ? old[j - 2] : B[j - 2]) : 0u;
+        } else {
+            for (int j = W - 1; j >= 0; --j) B[j] = j >= 2 ? B[j - 2] : 0u;
+        }
+    }
+    if (L > T) return -kEBADMSG;
+    if (L == 0) return 0;
+    if (!C[L]) return -kEBADMSG;
+    uint32_t P[kBigT];
+    int nr;
+    if (L == 1) {
+        P[0] = f.lg[C[1]];
+        nr = 1;
+    } else if (L <= 4) {
+        uint32_t X[4];
+        nr = small_roots(f, b.m, L, C[1], C[2], C[3], L >= 4 ? C[4] : 0u, X);
+        for (int i = 0; i < nr && i < 4; ++i) P[i] = f.lg[X[i]];
+    } else {
+        nr = chien_big(f, C, L, nbits, P, T);
+    }
+    if (nr != L) return -kEBADMSG;
+    for (int i = 0; i < L; ++i) {
+        if (P[i] >= nbits) return -kEBADMSG;
+        const uint32_t e = nbits - 1 - P[i];
+        const uint32_t el = (e & ~7u) | (7u - (e & 7u));
+        int j = i;                          // insertion into the ascending list
+        while (j > 0 && loc[j - 1] > el) {
+            loc[j] = loc[j - 1];
+            --j;
+        }
+        loc[j] = el;
+    }
+    return L;
+}
+
+template <int NW>
+__global__ void __launch_bounds__(kThreads) k_bch_decode_big(DevBch b, BchArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    stage_tables(b, smem, true);
+    const uint8_t *row = a.ecc_only ? nullptr : block_rows(smem, b, true, a);
+    const size_t k = (size_t)blockIdx.x * kThreads + threadIdx.x;
+    if (k >= a.ncw) return;
+    if (8ull * a.len > (unsigned long long)(b.n - b.ecc_bits)) {   // decode_bch's length check
+        a.result[k] = -kEINVAL;
+        return;
+    }
+    uint8_t *d = a.ecc_only ? nullptr : a.wdata + k * a.dstride, *e = a.ecc + k * a.estride;
+    Rem<NW> r;
+    if (a.ecc_only) {
+#pragma unroll
+        for (int i = 0; i < NW; ++i) r.w[i] = 0;
+    } else {
+        r = data_remainder<NW>(reinterpret_cast<const uint64_t *>(smem), row, a.len);
+    }
+    for (int i = 0; i < b.ecc_bytes && (i >> 3) < NW; ++i)    // bytes past NW words: unused bits
+        r.w[i >> 3] ^= (uint64_t)e[i] << (56 - 8 * (i & 7));
+    uint64_t any = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) any |= r.w[i];
+    if (!any) {
+        a.result[k] = 0;
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < NW; ++i) r.w[i] &= b.emask[i];
+    const uint16_t *sx = reinterpret_cast<const uint16_t *>(smem + tabs_offset(b));
+    const GF f{b.lds_tabs ? sx : b.ex, b.lds_tabs ? sx + 2 * b.n : b.lg, b.n};
+    uint32_t loc[kBigT];
+    const int cnt = locate_big<NW>(b, f, r, 8u * a.len + (uint32_t)b.ecc_bits, loc);
+    a.result[k] = cnt;
+    for (int i = 0; i < cnt; ++i) {
+        const uint32_t el = loc[i];
+        if (a.errloc) a.errloc[k * a.lstride + i] = el;
+        if (a.ecc_only) continue;
+        if (el < 8u * a.len) d[el >> 3] ^= (uint8_t)(1u << (el & 7));
+        else e[(el >> 3) - a.len] ^= (uint8_t)(1u << (el & 7));
+    }
+}
+
 hipError_t launch_encode(const DevBch &b, BchArgs a, hipStream_t s) {
     const unsigned grid = (unsigned)((a.ncw + kThreads - 1) / kThreads);
     a.staged = want_staging(b, false, a);
     const size_t sh = lds_bytes(b, false, a);
     if (b.nw == 1) hipLaunchKernelGGL(k_bch_encode<1>, dim3(grid), dim3(kThreads), sh, s, b, a);
     else if (b.nw == 2) hipLaunchKernelGGL(k_bch_encode<2>, dim3(grid), dim3(kThreads), sh, s, b, a);
-    else hipLaunchKernelGGL(k_bch_encode<4>, dim3(grid), dim3(kThreads), sh, s, b, a);
+    else if (b.nw == 4) hipLaunchKernelGGL(k_bch_encode<4>, dim3(grid), dim3(kThreads), sh, s, b, a);
+    else if (b.nw == 8) hipLaunchKernelGGL(k_bch_encode<8>, dim3(grid), dim3(kThreads), sh, s, b, a);
+    else hipLaunchKernelGGL(k_bch_encode<16>, dim3(grid), dim3(kThreads), sh, s, b, a);
     return hipGetLastError();
 }
 
@@ -506,7 +667,13 @@ hipError_t launch_decode(const DevBch &b, BchArgs a, hipStream_t s) {
     EZBCH_CASE(9, 4) EZBCH_CASE(10, 4) EZBCH_CASE(11, 4) EZBCH_CASE(12, 4) EZBCH_CASE(13, 4)
     EZBCH_CASE(14, 4) EZBCH_CASE(15, 4) EZBCH_CASE(16, 4)
 #undef EZBCH_CASE
-    return hipErrorInvalidValue;
+    // everything else init_bch accepts up to t = 64, ecc_bits = 1024
+    if (b.nw == 1) hipLaunchKernelGGL(k_bch_decode_big<1>, dim3(grid), dim3(kThreads), sh, s, b, a);
+    else if (b.nw == 2) hipLaunchKernelGGL(k_bch_decode_big<2>, dim3(grid), dim3(kThreads), sh, s, b, a);
+    else if (b.nw == 4) hipLaunchKernelGGL(k_bch_decode_big<4>, dim3(grid), dim3(kThreads), sh, s, b, a);
+    else if (b.nw == 8) hipLaunchKernelGGL(k_bch_decode_big<8>, dim3(grid), dim3(kThreads), sh, s, b, a);
+    else hipLaunchKernelGGL(k_bch_decode_big<16>, dim3(grid), dim3(kThreads), sh, s, b, a);
+    return hipGetLastError();
 }
 
 // ---- host --------------------------------------------------------------------------------------
@@ -587,7 +754,9 @@ struct HostBch {
         return true;
     }
 
-    unsigned words() const { return ecc_bits <= 64 ? 1 : ecc_bits <= 128 ? 2 : 4; }
+    unsigned words() const {
+        return ecc_bits <= 64 ? 1 : ecc_bits <= 128 ? 2 : ecc_bits <= 256 ? 4 : ecc_bits <= 512 ? 8 : 16;
+    }
     // step[v] = (v x^(E+8 nw 64-8) mod g) left-justified over nw words (w[0] most significant):
     // the remainder update for one data byte; laid out [v][word]
     std::vector<uint64_t> step_table() const {
@@ -645,8 +814,8 @@ int create_impl(ezbch_codec **out, unsigned m, unsigned t, unsigned poly, int de
         g_err = "BCH<N,K,T>: K does not match the codec init_bch builds (N - ecc_bits)";
         return -EINVAL;
     }
-    if (t > (unsigned)kMaxT || h.ecc_bits > 64u * kMaxNW) {
-        g_err = "BCH device path supports t <= 16 and ecc_bits <= 256";
+    if (t > (unsigned)kBigT || h.ecc_bits > 64u * kMaxNW) {
+        g_err = "BCH device path supports t <= 64 and ecc_bits <= 1024";
         return -ENOTSUP;
     }
     int ndev = 0;

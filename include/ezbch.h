@@ -18,7 +18,7 @@
  *
  * Bit conventions (bch_base:119-123): data bits enter MSB first; the ECC is the remainder
  * left-justified and big-endian in ecc_bytes bytes; an error location e addresses data[e/8] bit
- * (e%8) for e < 8*len and ECC byte e/8-len bit (e%8) beyond.  Device limits: t <= 16 and ecc_bits <= 256.
+ * (e%8) for e < 8*len and ECC byte e/8-len bit (e%8) beyond.  Device limit: t <= 64 (ecc_bits <= 1024).
  */
 #ifndef EZBCH_H
 #define EZBCH_H

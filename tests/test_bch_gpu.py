@@ -32,7 +32,9 @@ def _flip(rows, nbits, counts, rng):
 # (m, t): L <= 4 closed-form roots, L > 4 Chien, LDS and global field tables, unused ECC bits
 CODECS = [(5, 2), (8, 2), (8, 8), (10, 4), (11, 5), (12, 5), (13, 4), (15, 4), (7, 8),
           # beyond one 64-bit remainder word and t > 8 (general BCH)
-          (13, 8), (10, 9), (14, 12), (15, 16), (12, 16), (6, 10), (9, 13), (16 - 1, 9)]
+          (13, 8), (10, 9), (14, 12), (15, 16), (12, 16), (6, 10), (9, 13), (16 - 1, 9),
+          # t > 16 / ECC > 256 bits: the run-time-t kernel (k_bch_decode_big), 1..16 remainder words
+          (7, 17), (8, 17), (10, 20), (9, 30), (12, 30), (15, 40), (13, 64)]
 
 
 @pytest.mark.parametrize("m,t", CODECS, ids=[f"m{m}t{t}" for m, t in CODECS])
@@ -165,7 +167,7 @@ def test_c5_full_size_round_trip(torch):
     assert torch.equal(d, rows)
 
 
-@pytest.mark.parametrize("m,t", [(10, 4), (13, 8), (15, 16)])
+@pytest.mark.parametrize("m,t", [(10, 4), (13, 8), (15, 16), (13, 40)])
 def test_decode_from_ecc_difference(torch, m, t):
     """decode_bch's recv XOR calc form (bch_base:96-111; ezbch_decode_ecc): the locations found
     from the ECC difference alone equal those of a full decode of the same corrupted codeword."""

@@ -72,8 +72,8 @@ def test_bch_invalid_codecs_rejected_before_device():
     assert L.ezbch_create(C.byref(h), 4, 1, 0, 0) == -errno.EINVAL          # m < 5
     assert L.ezbch_create(C.byref(h), 5, 7, 0, 0) == -errno.EINVAL          # m*t >= n
     assert L.ezbch_create(C.byref(h), 8, 2, 0x101, 0) == -errno.EINVAL      # not primitive
-    assert L.ezbch_create(C.byref(h), 10, 17, 0, 0) == -errno.ENOTSUP       # valid, t > 16
-    assert L.ezbch_create(C.byref(h), 15, 20, 0, 0) == -errno.ENOTSUP       # valid, ECC > 256 bits
+    assert L.ezbch_create(C.byref(h), 10, 65, 0, 0) == -errno.ENOTSUP       # valid, t > 64
+    assert L.ezbch_create(C.byref(h), 15, 100, 0, 0) == -errno.ENOTSUP      # valid, t > 64
     assert L.ezbch_create_nkt(C.byref(h), 255, 240, 2, 0) == -errno.EINVAL  # BCH<255,240,2> mismatch
     assert L.ezbch_create_nkt(C.byref(h), 254, 239, 2, 0) == -errno.EINVAL
     assert not h.value
