@@ -65,6 +65,8 @@ struct BchArgs {
     size_t ncw;
     int staged;               // the block's data rows are copied to LDS with coalesced loads
     int ecc_only;             // decode_bch's "ecc = recv XOR calc" form: no data, nothing corrected
+    const uint32_t *syn;      // decode_bch's syndrome form: S_1..S_2t per codeword (ecc_only set)
+    size_t sstride;
 };
 
 constexpr size_t kLdsLimit = 65536;
@@ -315,17 +317,17 @@ __device__ __forceinline__ uint32_t coef(const uint32_t (&C)[W]) {
 // locations, or -EBADMSG.
 template <int T, int NW>
 __device__ int locate(const DevBch &b, const GF &f, Rem<NW> r, uint32_t nbits,
-                      uint32_t (&loc)[T]) {
+                      uint32_t (&loc)[T], const uint32_t *sin = nullptr) {
     uint64_t any = 0;
 #pragma unroll
     for (int i = 0; i < NW; ++i) any |= r.w[i];
-    if (!any) return 0;                     // only unused ECC bits differ
+    if (!any && !sin) return 0;             // only unused ECC bits differ
     const uint32_t n = (uint32_t)b.n;
     uint32_t S[2 * T + 1];
 #pragma unroll
-    for (int j = 0; j <= 2 * T; ++j) S[j] = 0;
+    for (int j = 0; j <= 2 * T; ++j) S[j] = (sin && j > 0) ? sin[j - 1] : 0u;
 #pragma unroll
-    for (int wi = 0; wi < NW; ++wi) {
+    for (int wi = 0; wi < NW && !sin; ++wi) {
         uint64_t x = r.w[wi];
         while (x) {                         // S_j = r(alpha^j), j odd
             const int lz = __clzll(x);
@@ -342,8 +344,10 @@ __device__ int locate(const DevBch &b, const GF &f, Rem<NW> r, uint32_t nbits,
             }
         }
     }
+    if (!sin) {
 #pragma unroll
-    for (int j = 1; j <= T; ++j) S[2 * j] = f.sq(S[j]);
+        for (int j = 1; j <= T; ++j) S[2 * j] = f.sq(S[j]);
+    }
 
     // Berlekamp-Massey; for a binary code the even-step discrepancies vanish.  B holds x^m B.
     constexpr int W = 2 * T + 2;
@@ -443,6 +447,19 @@ __global__ void __launch_bounds__(kThreads) k_bch_decode(DevBch b, BchArgs a) {
         a.result[k] = -kEINVAL;
         return;
     }
+    if (a.syn) {                                        // syndrome form: locations only
+        const uint16_t *sx = reinterpret_cast<const uint16_t *>(smem + tabs_offset(b));
+        const GF f{b.lds_tabs ? sx : b.ex, b.lds_tabs ? sx + 2 * b.n : b.lg, b.n};
+        Rem<NW> z;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) z.w[i] = 0;
+        uint32_t loc[T];
+        const int cnt = locate<T, NW>(b, f, z, 8u * a.len + (uint32_t)b.ecc_bits, loc, a.syn + k * a.sstride);
+        a.result[k] = cnt;
+        if (a.errloc)
+            for (int i = 0; i < cnt; ++i) a.errloc[k * a.lstride + i] = loc[i];
+        return;
+    }
     uint8_t *d = a.ecc_only ? nullptr : a.wdata + k * a.dstride, *e = a.ecc + k * a.estride;
     Rem<NW> r;
     if (a.ecc_only) {
@@ -506,17 +523,18 @@ __device__ int chien_big(const GF &f, const uint32_t *C, int L, uint32_t nbits, 
 
 // locate<T, NW> with run-time t <= kBigT
 template <int NW>
-__device__ int locate_big(const DevBch &b, const GF &f, Rem<NW> r, uint32_t nbits, uint32_t *loc) {
+__device__ int locate_big(const DevBch &b, const GF &f, Rem<NW> r, uint32_t nbits, uint32_t *loc,
+                          const uint32_t *sin = nullptr) {
     uint64_t any = 0;
 #pragma unroll
     for (int i = 0; i < NW; ++i) any |= r.w[i];
-    if (!any) return 0;
+    if (!any && !sin) return 0;
     const int T = b.t;
     const uint32_t n = (uint32_t)b.n;
     uint32_t S[2 * kBigT + 1];
-    for (int j = 0; j <= 2 * T; ++j) S[j] = 0;
+    for (int j = 0; j <= 2 * T; ++j) S[j] = (sin && j > 0) ? sin[j - 1] : 0u;
 #pragma unroll
-    for (int wi = 0; wi < NW; ++wi) {
+    for (int wi = 0; wi < NW && !sin; ++wi) {
         uint64_t x = r.w[wi];
         while (x) {                         // S_j = r(alpha^j), j odd
             const int lz = __clzll(x);
@@ -532,7 +550,8 @@ __device__ int locate_big(const DevBch &b, const GF &f, Rem<NW> r, uint32_t nbit
             }
         }
     }
-    for (int j = 1; j <= T; ++j) S[2 * j] = f.sq(S[j]);
+    if (!sin)
+        for (int j = 1; j <= T; ++j) S[2 * j] = f.sq(S[j]);
     // Berlekamp-Massey as in locate<T, NW>
     const int W = 2 * T + 2;
     uint32_t C[2 * kBigT + 2], B[2 * kBigT + 2], old[2 * kBigT + 2];
@@ -600,6 +619,19 @@ __global__ void __launch_bounds__(kThreads) k_bch_decode_big(DevBch b, BchArgs a
     if (k >= a.ncw) return;
     if (8ull * a.len > (unsigned long long)(b.n - b.ecc_bits)) {   // decode_bch's length check
         a.result[k] = -kEINVAL;
+        return;
+    }
+    if (a.syn) {                                        // syndrome form: locations only
+        const uint16_t *sx = reinterpret_cast<const uint16_t *>(smem + tabs_offset(b));
+        const GF f{b.lds_tabs ? sx : b.ex, b.lds_tabs ? sx + 2 * b.n : b.lg, b.n};
+        Rem<NW> z;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) z.w[i] = 0;
+        uint32_t loc[kBigT];
+        const int cnt = locate_big<NW>(b, f, z, 8u * a.len + (uint32_t)b.ecc_bits, loc, a.syn + k * a.sstride);
+        a.result[k] = cnt;
+        if (a.errloc)
+            for (int i = 0; i < cnt; ++i) a.errloc[k * a.lstride + i] = loc[i];
         return;
     }
     uint8_t *d = a.ecc_only ? nullptr : a.wdata + k * a.dstride, *e = a.ecc + k * a.estride;
@@ -995,6 +1027,21 @@ int ezbch_decode_ecc(const ezbch_codec *c, const uint8_t *ecc, size_t ecc_stride
     return e == hipSuccess ? 0 : hip_fail(e, "BCH decode launch");
 }
 
+int ezbch_decode_syn(const ezbch_codec *c, const uint32_t *syn, size_t syn_stride, unsigned len,
+                     int32_t *result, uint32_t *errloc, size_t errloc_stride, size_t ncw,
+                     void *stream) {
+    if (!c) return -EINVAL;
+    if (ncw == 0) return 0;
+    if (!result || !syn) return -EINVAL;
+    if (ncw > 1 && syn_stride < 2 * (size_t)c->h.t) return -EINVAL;
+    if (errloc && ncw > 1 && errloc_stride < c->h.t) return -EINVAL;
+    DeviceGuard g(c->device);
+    BchArgs a{nullptr, nullptr, 0, len, nullptr, 0, result, errloc, errloc_stride, ncw, 0, 1,
+              syn, syn_stride};
+    hipError_t e = launch_decode(c->dev, a, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? 0 : hip_fail(e, "BCH decode launch");
+}
+
 namespace {
 
 // Host encode: rows' data bytes go to the device (one linear copy of the span when the pitch is at
@@ -1056,6 +1103,33 @@ int ezbch_encode_rows_host(ezbch_codec *c, uint8_t *rows, size_t stride, unsigne
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard g(c->device);
     return bch_encode_host_core(c, rows, stride, len, rows + len, stride, ncw, chunk);
+}
+
+int ezbch_decode_syn_host(ezbch_codec *c, const uint32_t *syn, size_t syn_stride, unsigned len,
+                          int32_t *result, uint32_t *errloc, size_t errloc_stride, size_t ncw) {
+    if (!c) return -EINVAL;
+    if (ncw == 0) return 0;
+    if (!result || !syn) return -EINVAL;
+    const size_t S = 2 * (size_t)c->h.t, T = c->h.t;
+    if (ncw > 1 && syn_stride < S) return -EINVAL;
+    if (errloc && ncw > 1 && errloc_stride < T) return -EINVAL;
+    if (ncw == 1) syn_stride = S, errloc_stride = T;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    const size_t b_syn = align_up(ncw * S * 4), b_res = align_up(ncw * 4);
+    if (int r = ensure_stage(c, b_syn + b_res + ncw * T * 4)) return r;
+    uint8_t *st = static_cast<uint8_t *>(c->d_stage);
+    uint32_t *dsyn = reinterpret_cast<uint32_t *>(st);
+    int32_t *dres = reinterpret_cast<int32_t *>(st + b_syn);
+    uint32_t *dloc = reinterpret_cast<uint32_t *>(st + b_syn + b_res);
+    HIP_TRY(hipMemcpy2DAsync(dsyn, S * 4, syn, syn_stride * 4, S * 4, ncw, hipMemcpyHostToDevice, c->stream));
+    if (int r = ezbch_decode_syn(c, dsyn, S, len, dres, errloc ? dloc : nullptr, T, ncw, c->stream)) return r;
+    HIP_TRY(hipMemcpyAsync(result, dres, ncw * 4, hipMemcpyDeviceToHost, c->stream));
+    if (errloc)
+        HIP_TRY(hipMemcpy2DAsync(errloc, errloc_stride * 4, dloc, T * 4, T * 4, ncw, hipMemcpyDeviceToHost,
+                                 c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
 }
 
 int ezbch_decode_host(ezbch_codec *c, uint8_t *data, size_t data_stride, unsigned len,

@@ -95,6 +95,7 @@ def lib():
         L.ezbch_encode_rows_host.argtypes = [_vp, _vp, _sz, _u, _sz, _sz]
         L.ezbch_decode.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _vp, _vp, _sz, _sz, _vp]
         L.ezbch_decode_ecc.argtypes = [_vp, _vp, _sz, _u, _vp, _vp, _sz, _sz, _vp]
+        L.ezbch_decode_syn.argtypes = [_vp, _vp, _sz, _u, _vp, _vp, _sz, _sz, _vp]
         L.ezbch_encode_host.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _sz, _sz]
         L.ezbch_decode_host.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _vp, _vp, _sz, _sz, _sz]
         _lib = L
@@ -400,6 +401,20 @@ class BCH:
         _dev_rows(result, "result", self.device, 4, ndim=1)
         _check(lib().ezbch_decode_ecc(self._h, _tp(ecc), es, length, _tp(result), _tp(errloc), ls,
                                       ncw, _stream_ptr(stream)), "ezbch_decode_ecc", True)
+        return result
+
+    def decode_syn(self, syn, length, result=None, errloc=None, stream=None):
+        """decode_bch's syndrome form: syn rows hold S_1..S_2t (int32/uint32, 2t per row); returns
+        the int32 results; nothing is corrected (ezbch_decode_syn)."""
+        import torch
+        ncw = syn.shape[0]
+        ss = _dev_rows(syn, "syn", self.device, 4)
+        ls = _dev_rows(errloc, "errloc", self.device, 4)
+        if result is None:
+            result = torch.empty(ncw, dtype=torch.int32, device=syn.device)
+        _dev_rows(result, "result", self.device, 4, ndim=1)
+        _check(lib().ezbch_decode_syn(self._h, _tp(syn), ss, length, _tp(result), _tp(errloc), ls,
+                                      ncw, _stream_ptr(stream)), "ezbch_decode_syn", True)
         return result
 
     def encode_host(self, data, length=None, ecc=None, chunk=0):

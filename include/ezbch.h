@@ -77,6 +77,14 @@ int ezbch_decode_ecc(const ezbch_codec *codec, const uint8_t *ecc, size_t ecc_st
                      int32_t *result, uint32_t *errloc, size_t errloc_stride, size_t ncw,
                      void *stream);
 
+/* decode_bch's syndrome form (bch_base:112-114, "by providing syndrome results @syn"): syn rows
+ * hold S_1..S_2t (2t uint32 each, e.g. computed by hardware); result[k] = the number of errors
+ * those syndromes locate in a codeword of len data bytes (or -EBADMSG / -EINVAL), locations in
+ * errloc as ezbch_decode reports them; nothing is read or corrected.  Device pointers. */
+int ezbch_decode_syn(const ezbch_codec *codec, const uint32_t *syn, size_t syn_stride, unsigned len,
+                     int32_t *result, uint32_t *errloc, size_t errloc_stride, size_t ncw,
+                     void *stream);
+
 /* Host-memory forms (blocking), streamed through the device in chunks of `chunk` codewords
  * (0 = library default).  Encode moves only the data bytes in and a compact ECC block out; the
  * caller's data bytes are never written. */
@@ -87,6 +95,8 @@ int ezbch_encode_rows_host(ezbch_codec *codec, uint8_t *rows, size_t stride, uns
 int ezbch_decode_host(ezbch_codec *codec, uint8_t *data, size_t data_stride, unsigned len,
                       uint8_t *ecc, size_t ecc_stride, int32_t *result, uint32_t *errloc,
                       size_t errloc_stride, size_t ncw, size_t chunk);
+int ezbch_decode_syn_host(ezbch_codec *codec, const uint32_t *syn, size_t syn_stride, unsigned len,
+                          int32_t *result, uint32_t *errloc, size_t errloc_stride, size_t ncw);
 
 /* Human-readable text of the last BCH error seen by this thread ("" if none). */
 const char *ezbch_last_error(void);

@@ -140,17 +140,10 @@ void ezb_encode(const ezb_t *b, const uint8_t *data, unsigned len, uint8_t *ecc)
     free(r);
 }
 
-int ezb_decode(const ezb_t *b, const uint8_t *data, unsigned len, const uint8_t *recv,
-               unsigned *errloc) {
+/* S[1..2t] of the received codeword; returns 0 when recv equals the computed ECC (no syndromes) */
+static int syndromes(const ezb_t *b, const uint8_t *data, unsigned len, const uint8_t *recv, int *S) {
     const int n = b->n, t = b->t, E = b->ecc_bits;
-    if (8ull * len > (unsigned long long)(n - E)) return -EZB_EINVAL;
     uint8_t *r = malloc((size_t)E), *diff = malloc((size_t)b->ecc_bytes);
-    int *S = calloc(2 * (size_t)t + 1, sizeof(int));
-    const int W = 4 * t + 2;
-    int *elp = calloc((size_t)W, sizeof(int)), *pelp = calloc((size_t)W, sizeof(int)),
-        *cpy = calloc((size_t)W, sizeof(int));
-    unsigned *loc = calloc((size_t)t + 1, sizeof(unsigned));
-    int ret;
     lfsr_remainder(b, data, len, r);
     pack(b, r, diff);
     int any = 0;
@@ -158,14 +151,58 @@ int ezb_decode(const ezb_t *b, const uint8_t *data, unsigned len, const uint8_t 
         diff[i] ^= recv[i];
         any |= diff[i];
     }
-    if (!any) { ret = 0; goto out; }
+    memset(S, 0, sizeof(int) * (2 * (size_t)t + 1));
     /* S_j = diff(alpha^j) over the ecc_bits significant bits; bit i (MSB first) is x^(E-1-i) */
-    for (int i = 0; i < E; ++i) {
+    for (int i = 0; i < E && any; ++i) {
         if (!((diff[i >> 3] >> (7 - (i & 7))) & 1)) continue;
         const long long p = E - 1 - i;
         for (int j = 1; j < 2 * t; j += 2) S[j] ^= b->ex[(j * p) % n];
     }
     for (int j = 1; j <= t; ++j) S[2 * j] = gmul(b, S[j], S[j]);
+    free(r);
+    free(diff);
+    return any;
+}
+
+/* decode_bch's syndrome form (bch_base:96-114, "by providing syndrome results @syn"): the error
+ * locations from S_1..S_2t = syn[0..2t) alone */
+static int decode_from_syndromes(const ezb_t *b, unsigned len, const int *S, unsigned *errloc);
+
+int ezb_syndromes(const ezb_t *b, const uint8_t *data, unsigned len, const uint8_t *recv,
+                  unsigned *syn) {
+    int *S = calloc(2 * (size_t)b->t + 1, sizeof(int));
+    syndromes(b, data, len, recv, S);
+    for (int j = 1; j <= 2 * b->t; ++j) syn[j - 1] = (unsigned)S[j];
+    free(S);
+    return 0;
+}
+
+int ezb_decode_syn(const ezb_t *b, unsigned len, const unsigned *syn, unsigned *errloc) {
+    if (8ull * len > (unsigned long long)(b->n - b->ecc_bits)) return -EZB_EINVAL;
+    int *S = calloc(2 * (size_t)b->t + 1, sizeof(int));
+    for (int j = 1; j <= 2 * b->t; ++j) S[j] = (int)syn[j - 1];
+    const int r = decode_from_syndromes(b, len, S, errloc);
+    free(S);
+    return r;
+}
+
+int ezb_decode(const ezb_t *b, const uint8_t *data, unsigned len, const uint8_t *recv,
+               unsigned *errloc) {
+    if (8ull * len > (unsigned long long)(b->n - b->ecc_bits)) return -EZB_EINVAL;
+    int *S = calloc(2 * (size_t)b->t + 1, sizeof(int));
+    const int any = syndromes(b, data, len, recv, S);
+    const int r = any ? decode_from_syndromes(b, len, S, errloc) : 0;
+    free(S);
+    return r;
+}
+
+static int decode_from_syndromes(const ezb_t *b, unsigned len, const int *S, unsigned *errloc) {
+    const int n = b->n, t = b->t, E = b->ecc_bits;
+    const int W = 4 * t + 2;
+    int *elp = calloc((size_t)W, sizeof(int)), *pelp = calloc((size_t)W, sizeof(int)),
+        *cpy = calloc((size_t)W, sizeof(int));
+    unsigned *loc = calloc((size_t)t + 1, sizeof(unsigned));
+    int ret;
     /* Berlekamp-Massey, binary form: elp(x) = 1 + ... ; pelp = x^k-shifted previous elp */
     int edeg = 0, pdeg = 0, pp = -1, pd = 1, d = S[1];
     elp[0] = pelp[0] = 1;
@@ -216,7 +253,7 @@ int ezb_decode(const ezb_t *b, const uint8_t *data, unsigned len, const uint8_t 
     if (errloc) memcpy(errloc, loc, sizeof(unsigned) * (size_t)cnt);
     ret = cnt;
 out:
-    free(r); free(diff); free(S); free(elp); free(pelp); free(cpy); free(loc);
+    free(elp); free(pelp); free(cpy); free(loc);
     return ret;
 }
 

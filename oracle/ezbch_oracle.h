@@ -27,6 +27,11 @@ void ezb_genpoly(const ezb_t *b, uint8_t *coef);
 void ezb_encode(const ezb_t *b, const uint8_t *data, unsigned len, uint8_t *ecc);
 /* decode_bch(data, len, recv_ecc, NULL, NULL, errloc) (bch_base:86-127): the number of bit errors,
  * -74 (EBADMSG) or -22 (EINVAL); errloc[0..count) ascending. */
+/* S_1..S_2t (syn[0..2t)) of a received codeword; decode from syndromes alone (decode_bch's
+ * hardware-syndrome form) */
+int ezb_syndromes(const ezb_t *b, const uint8_t *data, unsigned len, const uint8_t *recv_ecc,
+                  unsigned *syn);
+int ezb_decode_syn(const ezb_t *b, unsigned len, const unsigned *syn, unsigned *errloc);
 int ezb_decode(const ezb_t *b, const uint8_t *data, unsigned len, const uint8_t *recv_ecc,
                unsigned *errloc);
 /* correct_bch (bch_base:168-199): decode, then flip the reported bits of data and ECC. */

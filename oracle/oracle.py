@@ -326,6 +326,8 @@ def _bch_lib():
         L.ezb_correct.argtypes = [_vp, _vp, _u, _vp, _vp]
         L.ezb_encode_batch.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _sz, _i]
         L.ezb_decode_batch.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _vp, _vp, _sz, _sz, _i]
+        L.ezb_syndromes.argtypes = [_vp, _vp, _u, _vp, _vp]
+        L.ezb_decode_syn.argtypes = [_vp, _u, _vp, _vp]
         _bch_ready = True
     return L
 
@@ -369,6 +371,21 @@ class BCH:
         """correct_bch in place on contiguous uint8 arrays; returns (result, error locations)."""
         loc = np.zeros(2 * self.t + 1, np.uint32)
         r = _bch_lib().ezb_correct(self._h, _ptr(data), len(data), _ptr(ecc), _ptr(loc))
+        return r, loc[:max(r, 0)].copy()
+
+    def syndromes(self, data, ecc):
+        """S_1..S_2t of (data, received ecc) as uint32[2t]."""
+        data = np.ascontiguousarray(data, np.uint8)
+        ecc = np.ascontiguousarray(ecc, np.uint8)
+        syn = np.zeros(2 * self.t, np.uint32)
+        _bch_lib().ezb_syndromes(self._h, _ptr(data), len(data), _ptr(ecc), _ptr(syn))
+        return syn
+
+    def decode_syn(self, length, syn):
+        """decode_bch's hardware-syndrome form: (result, ascending error locations)."""
+        syn = np.ascontiguousarray(syn, np.uint32)
+        loc = np.zeros(2 * self.t + 1, np.uint32)
+        r = _bch_lib().ezb_decode_syn(self._h, length, _ptr(syn), _ptr(loc))
         return r, loc[:max(r, 0)].copy()
 
     def encode_batch(self, data, length, ecc=None, nthreads=1):

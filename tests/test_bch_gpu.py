@@ -194,3 +194,60 @@ def test_decode_from_ecc_difference(torch, m, t):
     for k in np.nonzero(eres > 0)[0]:
         np.testing.assert_array_equal(got[k, :eres[k]], eloc[k, :eres[k]])
     np.testing.assert_array_equal(d.cpu().numpy(), diff)        # nothing corrected
+
+
+@pytest.mark.parametrize("m,t", [(10, 4), (13, 8), (15, 16), (10, 20), (13, 40)])
+def test_decode_from_syndromes(torch, m, t):
+    """decode_bch's syndrome form (bch_base:112-114; ezbch_decode_syn): syndromes of corrupted
+    codewords give the same locations as a full decode, and arbitrary syndrome vectors (not those
+    of any received word) give the oracle's result and locations."""
+    import ezrs
+    oc, c = O.BCH(m, t), ezrs.BCH(m, t)
+    rng = np.random.default_rng(31 * m + t)
+    L, eb = min(oc.max_len, 150), oc.ecc_bytes
+    ncw = 1200
+    ref = rng.integers(0, 256, (ncw, L + eb), dtype=np.uint8)
+    oc.encode_batch(ref, L)
+    bad = ref.copy()
+    _flip(bad, 8 * L + oc.ecc_bits, np.arange(ncw) % (t + 3), rng)
+    syn = np.stack([oc.syndromes(bad[k, :L], bad[k, L:]) for k in range(ncw)])
+    syn[ncw // 2:] = rng.integers(0, oc.n + 1, (ncw - ncw // 2, 2 * t))   # arbitrary vectors
+    syn[-7:] = 0                                                           # all-zero syndromes
+    exp = [oc.decode_syn(L, syn[k]) for k in range(ncw)]
+    d = torch.from_numpy(syn.view(np.int32)).cuda()
+    loc = torch.zeros((ncw, t), dtype=torch.int32, device="cuda")
+    res = c.decode_syn(d, L, errloc=loc).cpu().numpy()
+    np.testing.assert_array_equal(res, [r for r, _ in exp])
+    got = loc.cpu().numpy().view(np.uint32)
+    for k in range(ncw):
+        if exp[k][0] > 0:
+            np.testing.assert_array_equal(got[k, :exp[k][0]], exp[k][1])
+    full = bad[:ncw // 2].copy()
+    assert (res[:ncw // 2] == oc.decode_batch(full, L)).all()
+
+
+def test_decode_syn_host_form(torch):
+    """ezbch_decode_syn_host (the classic decode_bch(..., syn, errloc) behind include/ezpwd/bch):
+    host syndrome rows in, results and locations out, equal to the oracle."""
+    import ctypes as C
+    import ezrs
+    m, t, L = 10, 4, 100
+    oc, c = O.BCH(m, t), ezrs.BCH(m, t)
+    rng = np.random.default_rng(5)
+    ncw = 64
+    ref = rng.integers(0, 256, (ncw, L + oc.ecc_bytes), dtype=np.uint8)
+    oc.encode_batch(ref, L)
+    _flip(ref, 8 * L + oc.ecc_bits, np.arange(ncw) % (t + 3), rng)
+    syn = np.ascontiguousarray(np.stack([oc.syndromes(ref[k, :L], ref[k, L:]) for k in range(ncw)]))
+    res = np.zeros(ncw, np.int32)
+    loc = np.zeros((ncw, t), np.uint32)
+    L_ = ezrs.lib()
+    L_.ezbch_decode_syn_host.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint, C.c_void_p,
+                                         C.c_void_p, C.c_size_t, C.c_size_t]
+    assert L_.ezbch_decode_syn_host(c._h, syn.ctypes.data, 2 * t, L, res.ctypes.data, loc.ctypes.data,
+                                    t, ncw) == 0
+    for k in range(ncw):
+        er, el = oc.decode_syn(L, syn[k])
+        assert res[k] == er
+        if er > 0:
+            np.testing.assert_array_equal(loc[k, :er], el)
