@@ -657,7 +657,7 @@ def emit_fold_epilogue(out, gf, fname, T, nlw_expr, seq):
         if k == 0:
             prev[li] = (f"{T}[{li}]", 0)
             return f"{T}[{li}]"
-        src, kp = prev[li]
+        src, kp = prev.get(li, (f"{T}[{li}]", 0))
         direct = cost(sqk(k))
         chained = cost(sqk(k - kp)) if kp else direct
         out.append(f"{ind}uint32_t W{m}[8];")
@@ -989,6 +989,279 @@ def gen_pz(c: PsCodec):
     return "\n".join(out)
 
 
+# ---- tile kernel (k_pt): 8 waves share one 256-codeword tile ------------------------------------
+PT_WAVES = 8
+PT_XCAP = 3               # items (8 words each) a wave sends per exchange sub-round (48 KiB area)
+
+
+def pt_exchange(groups_need, qn):
+    """Recursive-halving reduce-scatter over the qn position-split waves of one item group.
+    groups_need[q] = set of item slots wave q needs at the end.  Round r pairs q with q ^ (1 << r);
+    after round r wave q holds the sums over its 2^(r+1)-wave block of the items needed by the
+    waves that agree with q on bits 0..r.  Returns per wave, per round (send list, recv list)."""
+    rounds = qn.bit_length() - 1
+    allitems = set().union(*groups_need) if groups_need else set()
+
+    def resp(q, r):                     # items wave q must hold after round r (r = -1: all)
+        if r < 0:
+            return set(allitems)
+        mask = (1 << (r + 1)) - 1
+        return set().union(*[groups_need[x] for x in range(qn) if (x & mask) == (q & mask)])
+    plan = []
+    for q in range(qn):
+        per = []
+        for r in range(rounds):
+            p = q ^ (1 << r)
+            send = sorted(resp(p, r) & resp(q, r - 1))
+            recv = sorted(resp(q, r) & resp(p, r - 1))
+            per.append((send, recv))
+        plan.append(per)
+    return plan
+
+
+def pt_xcost(plan, qn):
+    rounds = qn.bit_length() - 1
+    return sum(max(-(-len(plan[q][r][0]) // PT_XCAP) for q in range(qn)) for r in range(rounds))
+
+
+class PtRole:
+    """One direction of the tile kernel for one codec: items (decode: coset leaders; encode: parity
+    symbols) of 8 state words each, split into GN groups of NI items; each group's QN = 8 / GN
+    waves split the positions; a recursive-halving exchange leaves every wave the totals of the
+    items its epilogue folds (seq = [(item slot, output index, squarings)])."""
+
+    def __init__(self, c: PsCodec, enc: bool):
+        from itertools import combinations, permutations
+        self.c, self.enc = c, enc
+        gf = c.gf
+        K = N - c.nr
+        self.hi = K if enc else N
+        if enc:
+            nitems = c.nr
+            def G(p, j):
+                if p >= K:
+                    return 0
+                acc = 0
+                for i in range(c.nr):
+                    acc ^= gf.mul(c.Vinv[j][i], gf.pow_alpha(c.exps[i] * (N - 1 - p)))
+                return acc
+            self.wfun = [(lambda p, j=j: G(p, j)) for j in range(nitems)]
+            outs = [[(j, 0)] for j in range(nitems)]            # item j -> output j, no squaring
+        else:
+            nitems = len(c.leaders)
+            self.wfun = [(lambda p, l=l: c.w(l, p) if p < N else 0) for l in c.leaders]
+            outs = [sorted(c.members[l], key=lambda x: x[1]) for l in c.leaders]
+        self.gn = max(1, -(-nitems // 8))
+        while PT_WAVES % self.gn:
+            self.gn += 1
+        self.qn = PT_WAVES // self.gn
+        size = [len(o) for o in outs]
+        # 1. items -> GN groups of (nearly) equal item and output counts; 2. per group, outputs ->
+        #    QN waves by recursive halving of the group's output multiset, which is the exchange's
+        #    own structure: at each level choose how many outputs of every item go to each half
+        #    (equal output counts), minimising the distinct items per half (what the exchange
+        #    round of that level sends).  The group split is chosen by the resulting exchange cost.
+        from functools import lru_cache
+        from itertools import product
+        items = list(range(nitems))
+
+        def split(counts, n):
+            """counts: tuple of (item, outputs); n waves -> (cost, [per-wave (item, outputs) lists]).
+            Halves take whole items, at most one item split between them."""
+            if n == 1:
+                return (len(counts),), [list(counts)]
+            tot = sum(k for _, k in counts)
+            half = -(-tot // 2)
+            m = len(counts)
+            best = None
+            for mask in range(1 << m):
+                inA = [k for j, (_, k) in enumerate(counts) if mask >> j & 1]
+                sa = sum(inA)
+                opts = []
+                if sa == half:
+                    opts.append(None)
+                elif sa < half:
+                    for j, (_, k) in enumerate(counts):      # split item j: half - sa of it to A
+                        if not (mask >> j & 1) and k > half - sa:
+                            opts.append((j, half - sa))
+                for o in opts:
+                    A, B = [], []
+                    for j, (i, k) in enumerate(counts):
+                        if o is not None and o[0] == j:
+                            A.append((i, o[1]))
+                            B.append((i, k - o[1]))
+                        elif mask >> j & 1:
+                            A.append((i, k))
+                        else:
+                            B.append((i, k))
+                    here = max(len(A), len(B))
+                    if best is not None and here > best[0][0]:
+                        continue
+                    ca, ga = split(tuple(A), n // 2)
+                    cb, gb = split(tuple(B), n // 2)
+                    key = (here,) + tuple(max(x, y) for x, y in zip(ca, cb))
+                    if best is None or key < best[0]:
+                        best = (key, ga + gb)
+            return best
+
+        def plan_group(gitems):
+            counts = tuple((s, size[i]) for s, i in enumerate(gitems))
+            _, parts = split(counts, self.qn)
+            # part j of the recursion: bit r from the top selects the half at level r; wave q meets
+            # q ^ 1 in round 0 (the top split), so q = bit-reverse(j)
+            nbits = self.qn.bit_length() - 1
+            bins, used = [None] * self.qn, {}
+            for j, part in enumerate(parts):
+                q = int(format(j, f"0{nbits}b")[::-1], 2) if nbits else 0
+                b = []
+                for s, k in part:
+                    u = used.get(s, 0)
+                    b += [(s, m, kk) for m, kk in outs[gitems[s]][u:u + k]]
+                    used[s] = u + k
+                bins[q] = b
+            plan = pt_exchange([set(s for s, _, _ in b) for b in bins], self.qn)
+            return (pt_xcost(plan, self.qn), max(-(-len(b) // 4) for b in bins),
+                    sum(len(x[0]) for pq in plan for x in pq)), bins, plan
+
+        if self.gn == 1:
+            cands = [[items]]
+        elif enc:
+            per = -(-nitems // self.gn)
+            cands = [[items[i:i + per] for i in range(0, nitems, per)]]
+        else:
+            per = -(-nitems // self.gn)
+            target = sum(size) / self.gn
+            cands = []
+            assert self.gn == 2, "decode tile plan: at most two leader groups"
+            for comb in combinations(items[1:], per - 1):
+                grp = [0] + list(comb)
+                if sum(size[i] for i in grp) == round(target):
+                    cands.append([grp, [i for i in items if i not in grp]])
+                if len(cands) >= 60:
+                    break
+            if not cands:
+                cands = [[items[0::2], items[1::2]]]
+        best = None
+        for groups in cands:
+            res = [plan_group(gi) for gi in groups]
+            key = tuple(max(r[0][x] for r in res) for x in range(3))
+            if best is None or key < best[0]:
+                best = (key, groups, res)
+        _, groups, res = best
+        self.groups = groups
+        self.ni = max(len(g) for g in groups)
+        self.waves = {}                                       # wave -> dict
+        for g, (gitems, (_, bins, plan)) in enumerate(zip(groups, res)):
+            for q in range(self.qn):
+                w = g + self.gn * q
+                seq = bins[q]
+                own = sorted(set(s for s, _, _ in seq))
+                self.waves[w] = {"g": g, "q": q, "plan": plan[q], "own": own,
+                                 "seq": [(own.index(s), m, k) for s, m, k in seq]}
+        self.rounds = self.qn.bit_length() - 1
+        # sub-rounds: <= PT_XCAP items per wave at a time (the exchange area)
+        self.subs = []                                        # (round, chunk index)
+        for r in range(self.rounds):
+            nch = max(-(-len(self.waves[w]["plan"][r][0]) // PT_XCAP) for w in range(PT_WAVES))
+            self.subs += [(r, ch) for ch in range(nch)]
+        self.nown = max(1, max(len(v["own"]) for v in self.waves.values()))
+        self.nq = max(1, max(-(-len(v["seq"]) // 4) for v in self.waves.values()))
+        # 4. pieces (16 positions) per wave: half 0 = pieces 0..7, half 1 = 8..; round-robin
+        npieces = -(-self.hi // 16)
+        self.pieces = {}
+        for w in range(PT_WAVES):
+            q = self.waves[w]["q"]
+            h0 = [p for p in range(0, min(8, npieces)) if p % self.qn == q % self.qn]
+            h1 = [p for p in range(8, npieces) if (p - 8) % self.qn == q % self.qn]
+            self.pieces[w] = (h0, h1)
+
+
+def gen_pt(c: PsCodec):
+    """Tile-kernel tables and straight-line code, PT_<codec>: syndromes by coset leaders, the
+    leaders split into GN groups, the positions into QN quarters.  Wave (g, q) reads pieces
+    q, q + QN, q + 2 QN, ... and runs the networks of quarter 0's pieces on them -- so one network
+    set per group serves every quarter and the kernel's code stays small enough for the
+    instruction cache -- then multiplies its partials by alpha^(-16 q e) (fix<G, Q>): the weights
+    of position p + 16 q are alpha^(-16 q e) times those of position p.  Encode evaluates the same
+    syndromes over the data positions (the kernel masks positions >= K) for k_ps_parity8."""
+    out = []
+    R = PtRole(c, False)
+    st = f"PT_{c.name}"
+    W = PT_WAVES
+    mp = max(max(len(R.pieces[w][0]) + len(R.pieces[w][1]) for w in range(W)), 1)
+    nsub = max(len(R.subs), 1)
+
+    def pad(xs, n, v=-1):
+        return list(xs) + [v] * (n - len(xs))
+    X = PT_XCAP
+    xs = [[pad(R.waves[w]["plan"][r][0][X * ch:X * ch + X], X) for (r, ch) in R.subs] or [[-1] * X]
+          for w in range(W)]
+    xv = [[pad(R.waves[w]["plan"][r][1][X * ch:X * ch + X], X) for (r, ch) in R.subs] or [[-1] * X]
+          for w in range(W)]
+    syn = [[[R.waves[w]["seq"][4 * qd + j][1] if 4 * qd + j < len(R.waves[w]["seq"]) else -1
+             for j in range(4)] for qd in range(R.nq)] for w in range(W)]
+    for w in range(W):                                  # pieces of wave (g, q) = quarter 0's + q
+        q = R.waves[w]["q"]
+        p0 = R.pieces[R.waves[w]["g"]][0] + R.pieces[R.waves[w]["g"]][1]
+        mine = R.pieces[w][0] + R.pieces[w][1]
+        assert mine == [p + q for p in p0][:len(mine)], (w, mine, p0)
+    hdr = [f"struct {st} {{",
+           f"    static constexpr unsigned POLY = {c.poly:#x}, FCR = {c.fcr}, PRIM = {c.prim}, NR = {c.nr};",
+           f"    static constexpr int GN = {R.gn}, QN = {R.qn}, NI = {R.ni}, NOWN = {R.nown}, NQ = {R.nq};",
+           f"    static constexpr int NSUB = {len(R.subs)}, MP = {mp}, XCAP = {X};",
+           "    // pieces (16 positions) of wave W: NP0 in half 0, then NP1 in half 1 (decode: 255",
+           "    // positions; encode stops at the data positions)",
+           f"    static constexpr int NP0[{W}] = {fmt_list([len(R.pieces[w][0]) for w in range(W)])};",
+           f"    static constexpr int NP1[{W}] = {fmt_list([len(R.pieces[w][1]) for w in range(W)])};",
+           f"    static constexpr int PIECE[{W}][{mp}] = " + "{" + ", ".join(
+               fmt_list(pad(R.pieces[w][0] + R.pieces[w][1], mp)) for w in range(W)) + "};",
+           "    // exchange sub-round s (round XR[s]): wave W sends item slots XS[W][s], adds the",
+           "    // partner's words into slots XV[W][s] (partner = W ^ (GN << XR[s]))",
+           f"    static constexpr int XR[{nsub}] = {fmt_list([r for r, _ in R.subs] or [0])};",
+           f"    static constexpr int XS[{W}][{nsub}][{X}] = " + "{" + ", ".join(
+               "{" + ", ".join(fmt_list(x) for x in xs[w]) + "}" for w in range(W)) + "};",
+           f"    static constexpr int XV[{W}][{nsub}][{X}] = " + "{" + ", ".join(
+               "{" + ", ".join(fmt_list(x) for x in xv[w]) + "}" for w in range(W)) + "};",
+           "    // item slots whose totals wave W folds (T[i] <-> slot OWN[W][i])",
+           f"    static constexpr int OWN[{W}][{R.nown}] = " + "{" + ", ".join(
+               fmt_list(pad(R.waves[w]["own"], R.nown)) for w in range(W)) + "};",
+           "    // syndrome index of quad slot (W, quad, j), -1 = none",
+           f"    static constexpr int SYN[{W}][{R.nq}][4] = " + "{" + ", ".join(
+               "{" + ", ".join(fmt_list(q) for q in syn[w]) + "}" for w in range(W)) + "};",
+           "    // positions 8B..8B+7 (words X) into group G's state, B a block of quarter 0",
+           "    template <int G, int B> static __device__ void block(uint32_t (&V)[NI][8], const uint32_t (&X)[8]);",
+           "    // group G's partials of quarter Q (computed with quarter 0's weights) times alpha^(-16 Q e)",
+           "    template <int G, int Q> static __device__ void fix(uint32_t (&V)[NI][8]);",
+           "    template <int W, class F> static __device__ void epilogue(const uint32_t (&T)[NOWN][8], F &&emit);",
+           "};"]
+    out += hdr
+    gf = c.gf
+    for g, gitems in enumerate(R.groups):
+        ws = [R.wfun[i] for i in gitems]
+        p0 = R.pieces[g][0] + R.pieces[g][1]            # wave (g, 0) = wave g
+        for pc in p0:
+            for B in (2 * pc, 2 * pc + 1):
+                emit_weight_block(out, f"template <> __device__ __forceinline__ void {st}::block<{g}, {B}>("
+                                  "uint32_t (&V)[NI][8], const uint32_t (&X)[8])", ws, B)
+        for q in range(1, R.qn):
+            out.append(f"template <> __device__ __forceinline__ void {st}::fix<{g}, {q}>(uint32_t (&V)[NI][8]) {{")
+            out.append("    uint32_t t[8];")
+            for s, i in enumerate(gitems):
+                e = c.exps[c.leaders[i]]
+                cst = gf.pow_alpha((-16 * q * e) % N)
+                rows = lin_rows(lambda x, cst=cst: gf.mul(cst, x))
+                out.append(f"    for (int b = 0; b < 8; ++b) t[b] = V[{s}][b];")
+                mat_apply(out, [f"V[{s}][{b}]" for b in range(8)], [f"t[{b}]" for b in range(8)], rows, "    ")
+            out.append("}")
+    for w in range(W):
+        emit_fold_epilogue(out, c.gf, f"{st}_epi{w}", "T", f"{st}::NOWN", R.waves[w]["seq"])
+    out.append(f"template <int W, class F> __device__ __forceinline__ void {st}::epilogue("
+               "const uint32_t (&T)[NOWN][8], F &&emit) {")
+    out.append("    " + " else ".join(f"if constexpr (W == {w}) {st}_epi{w}(T, emit);" for w in range(W)))
+    out.append("}")
+    return "\n".join(out)
+
+
 def main(dst=None):
     dst = dst or os.path.join(HERE, "..", "csrc", "gen", "ezrs_ps_tables.inc")
     os.makedirs(os.path.dirname(dst), exist_ok=True)
@@ -1004,7 +1277,7 @@ def main(dst=None):
         body.append(gen_codec(PsCodec(*cd)))
         body.append(gen_pw(PsCodec(*cd)))
         body.append(gen_py(PsCodec(*cd)))
-        body.append(gen_pg(PsCodec(*cd), 4))
+        body.append(gen_pt(PsCodec(*cd)))
 
     body.append("#define EZRS_PS_CODEC_LIST(X) \\")
     for i, cd in enumerate(CODECS):

@@ -326,6 +326,12 @@ __device__ int locate(const DevBch &b, const GF &f, Rem<NW> r, uint32_t nbits,
     uint32_t S[2 * T + 1];
 #pragma unroll
     for (int j = 0; j <= 2 * T; ++j) S[j] = (sin && j > 0) ? sin[j - 1] : 0u;
+    if (sin) {                              // a caller's syndrome outside GF(2^m) indexes no table
+        uint32_t bad = 0;
+#pragma unroll
+        for (int j = 1; j <= 2 * T; ++j) bad |= S[j] > n;
+        if (bad) return -EINVAL;
+    }
 #pragma unroll
     for (int wi = 0; wi < NW && !sin; ++wi) {
         uint64_t x = r.w[wi];
@@ -533,6 +539,11 @@ __device__ int locate_big(const DevBch &b, const GF &f, Rem<NW> r, uint32_t nbit
     const uint32_t n = (uint32_t)b.n;
     uint32_t S[2 * kBigT + 1];
     for (int j = 0; j <= 2 * T; ++j) S[j] = (sin && j > 0) ? sin[j - 1] : 0u;
+    if (sin) {                              // a caller's syndrome outside GF(2^m) indexes no table
+        uint32_t bad = 0;
+        for (int j = 1; j <= 2 * T; ++j) bad |= S[j] > n;
+        if (bad) return -EINVAL;
+    }
 #pragma unroll
     for (int wi = 0; wi < NW && !sin; ++wi) {
         uint64_t x = r.w[wi];
@@ -1051,8 +1062,10 @@ namespace {
 int bch_encode_host_core(ezbch_codec *c, const uint8_t *data, size_t data_stride, unsigned len,
                          uint8_t *ecc, size_t ecc_stride, size_t ncw, size_t chunk) {
     const size_t eb = c->h.ecc_bytes;
+    // a single row is staged at pitch len whatever its stride (a stride below len, 0 included, is
+    // legal for one codeword and must not size the staging)
     const bool span = ncw == 1 || data_stride <= 2 * (size_t)len + eb;
-    const size_t drow = span ? data_stride : len;
+    const size_t drow = ncw == 1 ? len : span ? data_stride : len;
     const bool ecc_direct = ecc_stride == eb || ncw == 1;
     if (!chunk) chunk = ((size_t)64 << 20) / (drow ? drow : 1) + 1;
     if (chunk > ncw) chunk = ncw;

@@ -496,7 +496,9 @@ int encode_host_core(ezrs_codec *c, const char *data, size_t data_stride, unsign
     const size_t w = c->dev.mm <= 8 ? 1 : 2, NR = c->dev.nroots;
     const size_t need = (size_t)len;                               // symbols a row must carry over
     const bool span = ncw == 1 || data_stride <= 2 * need + NR;    // linear copy of the rows' span
-    const size_t drow = span ? data_stride : need;                 // device row pitch (symbols)
+    // device row pitch (symbols); a single row is staged at pitch len whatever its stride (a stride
+    // below len, 0 included, is legal for one codeword and must not size the staging)
+    const size_t drow = ncw == 1 ? need : span ? data_stride : need;
     const bool par_direct = parity_stride == NR || ncw == 1;       // caller's parity is compact
     if (!chunk) chunk = default_chunk(drow * w);
     if (chunk > ncw) chunk = ncw;

@@ -74,9 +74,11 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
     // syndromes (polynomial form from the syndrome kernel) -> logs, stored reversed (1416-1434)
     unsigned syn_error = 0;
     {
-        uint4 w0, w1;
-        __builtin_memcpy(&w0, syn_in, 16);
-        __builtin_memcpy(&w1, syn_in + 16, 16);
+        uint4 w0 = make_uint4(0, 0, 0, 0), w1 = w0;
+        if (syn_in) {
+            __builtin_memcpy(&w0, syn_in, 16);
+            __builtin_memcpy(&w1, syn_in + 16, 16);
+        }
         const unsigned w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
 #pragma unroll
         for (int i = 0; i < 32; ++i) {
@@ -260,6 +262,9 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
 }
 
 // Screen span `sp`: the flagged slots' offsets into `list` (when given), their number returned.
+// A slot is flagged when the syndrome kernel left the sentinel in it (nonzero syndromes) or when
+// the codeword carries erasures (the reference validates them before the zero-syndrome return,
+// rs_base:1375-1387; a slot holding 0 then means all-zero syndromes).
 __device__ __forceinline__ unsigned screen(const DecodeArgs &a, size_t sp, unsigned lane, uint16_t *list) {
     const size_t k0 = sp * kSpan + 4 * lane;
     unsigned mine = 0;
@@ -271,6 +276,16 @@ __device__ __forceinline__ unsigned screen(const DecodeArgs &a, size_t sp, unsig
     } else {
         for (int i = 0; i < 4; ++i)
             if (k0 + i < a.ncw && a.result[k0 + i] == kSentinel) mine |= 1u << i;
+    }
+    if (a.neras) {
+        if (k0 + 4 <= a.ncw && (reinterpret_cast<uintptr_t>(a.neras + k0) & 15) == 0) {
+            uint4 e;
+            __builtin_memcpy(&e, a.neras + k0, 16);
+            mine |= (e.x != 0) | (e.y != 0) << 1 | (e.z != 0) << 2 | (e.w != 0) << 3;
+        } else {
+            for (int i = 0; i < 4; ++i)
+                if (k0 + i < a.ncw && a.neras[k0 + i]) mine |= 1u << i;
+        }
     }
     // entry (lane, bit) goes to base_bit + (lanes below with that bit)
     unsigned nflag = 0;
@@ -323,8 +338,11 @@ __global__ void __launch_bounds__(64 * kWaves) k_decode_errors(DevCodec c, Decod
                 const unsigned ne = a.neras ? a.neras[k] : 0;
                 uint32_t *pos = a.positions ? a.positions + k * a.pos_stride : nullptr;
                 uint8_t *corr = a.corr ? static_cast<uint8_t *>(a.corr) + k * a.corr_stride : nullptr;
+                // a slot that does not hold the sentinel was flagged for its erasures only: its
+                // syndromes are zero and were not written
+                const bool synz = a.result[k] != kSentinel;
                 a.result[k] = decode_lane(c, L, W, lane, data, a.len, parity, eras, ne, pos, corr,
-                                          syn_ws + k * 32);
+                                          synz ? nullptr : syn_ws + k * 32);
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // list reads done before the next span
@@ -339,7 +357,8 @@ hipError_t launch_decode_flagged(const DevCodec &c, const DecodeArgs &a, const u
     if (c.mm != 8 || c.nroots > 32 || c.masked) return hipErrorInvalidValue;
     const size_t nspan = (a.ncw + kSpan - 1) / kSpan;
     const size_t want = (nspan + kWaves - 1) / kWaves;
-    const unsigned grid = (unsigned)(want < (size_t)c.ncu ? want : (size_t)c.ncu);
+    const size_t ncu = c.ncu > 0 ? (size_t)c.ncu : 256;    // attribute query failed: assume 256
+    const unsigned grid = (unsigned)(want < ncu ? want : ncu);
     hipLaunchKernelGGL(k_decode_errors, dim3(grid), dim3(64 * kWaves), 0, s, c, a, syn_ws);
     return hipGetLastError();
 }

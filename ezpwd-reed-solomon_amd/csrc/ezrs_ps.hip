@@ -1,67 +1,59 @@
-// ezrs_ps.hip -- plane-sliced GF(2^8) RS syndrome kernels for MI355X (gfx950).
+// ezrs_ps.hip -- plane-sliced GF(2^8) RS kernels for MI355X (gfx950): syndromes (decode) and
+// parity (encode) of batches of 255-symbol codewords.
 //
-// Computes the syndromes S_i = r(alpha^((fcr+i)*prim)) of c++/ezpwd/rs_base:1390-1414 for batches
-// of 255-symbol codewords.  Decode: a codeword whose syndromes are all zero (and that carries no
-// erasures) gets result 0, exactly decode_symbols' early return (rs_base:1416-1434); every other
-// codeword gets a sentinel and its syndromes go to the workspace for the error path
-// (ezrs_generic.hip: k_decode_flagged).  Encode: the syndromes of the data symbols go to a
-// workspace and k_ps_parity maps them to parity (parity = V^-1 S).
+// Decode computes the syndromes S_i = r(alpha^((fcr+i)*prim)) of c++/ezpwd/rs_base:1390-1414.  A
+// codeword whose syndromes are all zero (and that carries no erasures) gets result 0, exactly
+// decode_symbols' early return (rs_base:1416-1434); every other codeword gets a sentinel and its
+// syndromes go to the workspace for the error path (ezrs_errors.hip: k_decode_errors).  Encode
+// computes the parity of encode_symbols (rs_base:1296-1332) directly from the data symbols.
 //
 // Arithmetic (codegen/gen_ps.py has the derivation): a 32-bit word holds one position of four
-// codewords, bit 8k + b = bit-plane b of codeword k.  Each bit is a GF(2) stream, so only one root
-// per cyclotomic coset ("leader") is evaluated -- V_{b,2e} = V_{b,e}^2 -- and the per-plane values
-// are folded into syndromes (S = sum_b alpha^b V_b) once per tile.  For RS(255,223) the main loop
-// keeps 16 leaders x 8 bits = 128 state words per codeword slot set, half the state (and half the
-// XORs per input symbol) of a per-symbol bit-slicing of the 32 syndromes.
+// codewords, bit 8k + b = bit-plane b of codeword k.  Each bit is a GF(2) stream.
+//   * decode: only one root per cyclotomic coset ("leader") is evaluated -- V_{b,2e} = V_{b,e}^2 --
+//     and the per-plane values are expanded and folded into syndromes (S = sum_b alpha^b V_b) once
+//     per tile: 16 leaders x 8 bits for RS(255,223);
+//   * encode: parity_j = sum_b alpha^b P_{b,j}, P_{b,j} = sum_p bit_b(d_p) G[p][j] with the
+//     systematic generator weights G[p][j] = sum_i Vinv[j][i] alpha^(e_i (N-1-p)): no syndromes,
+//     no parity pass, no workspace.
 //
-// Work decomposition (one 512-thread workgroup per CU, persistent over tiles):
-//   * tile = 256 consecutive codewords; lane l of every wave owns codewords 4l..4l+3 of the tile.
-//   * the tile's rows are one contiguous span (row pitch <= 256 B): it is copied to LDS by linear
-//     1-KiB LDS-DMA instructions through a buffer resource (out-of-range bytes read as zero), double
-//     buffered: the next tile lands while this one is computed.  (Row-gather DMA shapes measured
-//     4.1-5.3 TB/s, whole-tile linear loads 6.2-6.7 TB/s: tools/micro/ps_stream2.hip.)
-//   * wave (g, q), g = wave / 4, q = wave % 4: leader group g (8 leaders, 64 state words) over
-//     position slice q (64 positions decode, 56 encode).  Each lane reads its 4 rows' bytes with
-//     aligned ds_read_b32 + v_alignbyte (gfx950 LDS does not serve unaligned reads), transposes
-//     4x4 bytes with v_perm, and runs the generated XOR networks.
-//   * slice q's partials are multiplied by alpha^(-q S e) and summed across the 4 slices through
-//     LDS (two pairwise exchange rounds in the consumed tile buffer); each wave then owns the
-//     totals of two leaders and runs their expansion + plane fold (generated epilogue).
-//   * global stores of a tile are issued after the next tile's top barrier, so the vmcnt wait of
-//     that barrier only covers memory operations issued a whole tile earlier.
+// Tile kernel k_pt (the default): one 512-thread workgroup (8 waves) per 256-codeword tile, two
+// workgroups per CU (80 KiB of LDS each, <= 128 VGPRs: 4 waves per SIMD), persistent over tiles.
+//   * The tile lands in LDS as two 32 KiB half images (positions 0..127, 128..255) by LDS-DMA of
+//     whole 128-byte row chunks (8 lanes per row, 8 rows per instruction) in an XOR-swizzled
+//     layout that makes every ds_read_b128 of the compute conflict-free.  The halves are
+//     pipelined: the next tile's half 0 is fetched while this tile's half 1 is computed, its half 1
+//     while this tile's epilogue runs.
+//   * Waves split the items (decode: leaders; encode: parity symbols, 8 state words each) into GN
+//     groups and the positions into QN = 8 / GN parts; lane l owns codewords l + 64k, k = 0..3 (byte
+//     k of its words).  Piece reads are software-pipelined (the next piece's ds_reads are in flight
+//     while the current one's second block runs).
+//   * A recursive-halving exchange through the consumed half-1 image (plus 16 KiB) leaves every
+//     wave the totals of the items its generated epilogue folds: decode, 4 syndromes (one quad) per
+//     wave; encode, 4 parity symbols per wave, stored straight into the codeword rows.
+//   * All LDS traffic, LDS-DMA and global stores are inline asm with counted s_waitcnt: the
+//     compiler would otherwise wait for every DMA in flight at each LDS access or barrier.  Stores
+//     and DMAs are issued unconditionally (out-of-range buffer offsets drop unwanted ones), so
+//     every vmcnt is a compile-time constant.
+//
+// k_py_syndromes + k_ps_parity8 (EZRS_PS_VARIANT=pair) are the round-2 kernels, kept for A/B runs.
 #include "ezrs_internal.hpp"
 #include "gen/ezrs_ps_tables.inc"
 
 namespace ezrs {
 namespace ps {
 
-constexpr int kThreads = 512;
-constexpr int kWaves = 8;
 constexpr int kTile = 256;                          // codewords per tile
-constexpr int kGuard = 256;                         // bytes before each tile image (pad reads)
-constexpr int kTileMax = 65536;                     // tile bytes: 256 rows x pitch <= 256 B
-constexpr int kBufBytes = kGuard + kTileMax + 64;
 constexpr int32_t kSentinel = INT32_MIN;
 constexpr int kN = 255;
 
 typedef __attribute__((address_space(3))) void lds_void;
 
-// Timing-only builds (tools/micro/ps_stamps.hip): per-phase s_memtime stamps of the first
-// workgroups.  Never defined in the library.
 #ifdef EZRS_PS_STAMPS
-__device__ unsigned long long g_ps_stamps[8][8][16][8];    // [wg][wave][tile][phase]
-#define PS_STAMP(ph) do { if (blockIdx.x < 8 && it < 16 && lane == 0) \
-    g_ps_stamps[blockIdx.x][wave][it][ph] = __builtin_amdgcn_s_memtime(); } while (0)
 __device__ unsigned long long g_py_stamps[16][2][8][8];  // [wg][wave][tile][phase]
-__device__ unsigned long long g_pg_stamps[16][8][16][8];  // [wg][wave][tile][phase]
-#define PG_STAMP(ph) do { __builtin_amdgcn_sched_barrier(0); if (blockIdx.x < 16 && it < 16 && lane == 0) \
-    g_pg_stamps[blockIdx.x][stamp_wave][it][ph] = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
 #define PY_STAMP(ph) do { __builtin_amdgcn_sched_barrier(0); if (blockIdx.x < 16 && it < 8 && lane == 0) \
     g_py_stamps[blockIdx.x][Q][it][ph] = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
 #else
-#define PS_STAMP(ph) do { } while (0)
 #define PY_STAMP(ph) do { } while (0)
-#define PG_STAMP(ph) do { } while (0)
 #endif
 
 struct PsArgs {
@@ -74,11 +66,13 @@ struct PsArgs {
     int hi;                     // one past the last evaluated position (255 decode, 255-NR encode)
     const uint32_t *neras;      // decode: erasure counts (nullable)
     int32_t *result;            // decode
-    uint8_t *ws;                // decode: [ncw][32] flagged syndromes; encode: [NR][ws_pitch]
-    size_t ws_pitch;            // encode: codewords per syndrome row (a multiple of 2048)
-    int ablate;                 // timing experiments only (tools/micro): bit 0 no main loop, 1 no
-                                // exchange, 2 no epilogue, 3 no DMA, 4 no result stores; 0 in the
-                                // library
+    uint8_t *ws;                // decode: [ncw][32] flagged syndromes; pair encode: [NR][ws_pitch]
+    size_t ws_pitch;            // pair encode: codewords per syndrome row (a multiple of 2048)
+    uint8_t *parity;            // tile encode: parity of codeword k at parity + k * pstride
+    uint32_t pstride;
+    uint32_t pspan;             // bytes writable from parity
+    int ablate;                 // timing experiments only (tools/pt_ablate.py, EZRS_PT_ABLATE): bit 0
+                                // no main loop, 1 no exchange, 2 no fold, 3 no DMA, 5 nothing flagged
 };
 
 template <int I, int N, class F> __device__ __forceinline__ void static_for(F &&f) {
@@ -114,294 +108,6 @@ __device__ __forceinline__ void transpose4x4(const uint32_t (&a)[4], uint32_t *o
     out[1] = __builtin_amdgcn_perm(t23, t01, 0x07060302u);
     out[2] = __builtin_amdgcn_perm(u23, u01, 0x05040100u);
     out[3] = __builtin_amdgcn_perm(u23, u01, 0x07060302u);
-}
-
-// Issue this wave's share of the tile's linear LDS-DMA (1 KiB per instruction).
-__device__ __forceinline__ void issue_tile(uint8_t *buf, const PsArgs &a, __amdgpu_buffer_rsrc_t rsrc,
-                                           uint32_t tile, int wave, int lane) {
-    const uint32_t tb = a.stride * kTile;                 // tile bytes
-    const uint32_t ninstr = (tb + 1023) >> 10;
-    const uint32_t t0 = tile * tb;
-    for (uint32_t i = wave; i < ninstr; i += kWaves)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void *)(buf + kGuard + i * 1024), 16,
-                                                 t0 + i * 1024 + 16 * lane, 0, 0, 0);
-}
-
-// The 8 position words of positions p0..p0+7 for the lane's 4 rows: X[t] byte k = row k symbol.
-__device__ __forceinline__ void load_block(const uint8_t *buf, const int (&rb)[4], const uint32_t (&sh)[4],
-                                           int p0, uint32_t (&X)[8]) {
-    uint32_t lo[4], hi[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int o = rb[k] + p0;                         // rb: row start - lo, relative to buf
-        const uint32_t *d = reinterpret_cast<const uint32_t *>(buf + (o & ~3));
-        const uint32_t d0 = d[0], d1 = d[1], d2 = d[2];
-        lo[k] = __builtin_amdgcn_alignbyte(d1, d0, sh[k]);
-        hi[k] = __builtin_amdgcn_alignbyte(d2, d1, sh[k]);
-    }
-    transpose4x4(lo, X);
-    transpose4x4(hi, X + 4);
-}
-
-// Main loop of one wave: group G over slice positions [q S, q S + S) (S = 8 NB).
-template <class C, int G, int NB>
-__device__ __forceinline__ void main_slice(uint32_t (&V)[C::NLG][8], const uint8_t *buf,
-                                           const int (&rb)[4], const uint32_t (&sh)[4], int s0,
-                                           int lo, int hi) {
-    static_for<0, NB>([&](auto B) {
-        const int p0 = s0 + 8 * B;                        // full-frame position of word X[0]
-        if (p0 + 8 > lo && p0 < hi) {                     // wave-uniform
-            uint32_t X[8];
-            load_block(buf, rb, sh, p0, X);
-            if (p0 < lo || p0 + 8 > hi) {
-#pragma unroll
-                for (int t = 0; t < 8; ++t)
-                    if (p0 + t < lo || p0 + t >= hi) X[t] = 0;
-            }
-            C::template block<G, decltype(B)::value>(V, X);
-        }
-    });
-}
-
-// Reduction of the slice partials: wave (g, q) ends with the totals of leader slots
-// 2 idx, 2 idx + 1 of group g, idx = 2 (q & 1) + (q >> 1)  (gen_ps.py assigns leaders to match).
-template <class C, int q>
-__device__ __forceinline__ void reduce(uint32_t (&V)[C::NLG][8], uint32_t (&T)[2][8], uint8_t *buf,
-                                       int wave, int lane) {
-    uint4 *r1 = reinterpret_cast<uint4 *>(buf);          // 8 waves x 8 x 1 KiB
-    // round 1: partner q ^ 1; keep slots [4 (q & 1), +4), send the other 4 (32 words)
-    constexpr int keep1 = 4 * (q & 1), send1 = 4 - keep1;
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int ss = send1 + s;
-            uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-            // select the slot at run time (wave-uniform) without dynamic register indexing
-#pragma unroll
-            for (int c = 0; c < 8; ++c)
-                if (c == ss) { w0 = V[c][4 * h]; w1 = V[c][4 * h + 1]; w2 = V[c][4 * h + 2]; w3 = V[c][4 * h + 3]; }
-            r1[(wave * 8 + 2 * s + h) * 64 + lane] = make_uint4(w0, w1, w2, w3);
-        }
-    __syncthreads();
-    const int partner1 = wave ^ 1;
-    uint32_t K[4][8];
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const uint4 v = r1[(partner1 * 8 + 2 * s + h) * 64 + lane];
-            uint32_t m0 = 0, m1 = 0, m2 = 0, m3 = 0;
-#pragma unroll
-            for (int c = 0; c < 8; ++c)
-                if (c == keep1 + s) { m0 = V[c][4 * h]; m1 = V[c][4 * h + 1]; m2 = V[c][4 * h + 2]; m3 = V[c][4 * h + 3]; }
-            K[s][4 * h] = m0 ^ v.x; K[s][4 * h + 1] = m1 ^ v.y;
-            K[s][4 * h + 2] = m2 ^ v.z; K[s][4 * h + 3] = m3 ^ v.w;
-        }
-    __syncthreads();                                      // r1 is read; round 2 reuses it
-    // round 2: partner q ^ 2; keep K slots [2 (q >> 1), +2), send the other 2 (16 words)
-    constexpr int keep2 = 2 * (q >> 1), send2 = 2 - keep2;
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-                if (c == send2 + s) { w0 = K[c][4 * h]; w1 = K[c][4 * h + 1]; w2 = K[c][4 * h + 2]; w3 = K[c][4 * h + 3]; }
-            r1[(wave * 4 + 2 * s + h) * 64 + lane] = make_uint4(w0, w1, w2, w3);
-        }
-    __syncthreads();
-    const int partner2 = wave ^ 2;
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const uint4 v = r1[(partner2 * 4 + 2 * s + h) * 64 + lane];
-            uint32_t m0 = 0, m1 = 0, m2 = 0, m3 = 0;
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-                if (c == keep2 + s) { m0 = K[c][4 * h]; m1 = K[c][4 * h + 1]; m2 = K[c][4 * h + 2]; m3 = K[c][4 * h + 3]; }
-            T[s][4 * h] = m0 ^ v.x; T[s][4 * h + 1] = m1 ^ v.y;
-            T[s][4 * h + 2] = m2 ^ v.z; T[s][4 * h + 3] = m3 ^ v.w;
-        }
-}
-
-// Deferred global stores of one tile (issued after the next tile's top barrier).
-template <class C> struct Pending {
-    uint32_t D[C::NQ][4];       // syndrome bytes of the lane's 4 codewords, per quad slot
-    uint32_t flags;             // decode: bit k = codeword 4 lane + k is flagged
-    int32_t res[4];
-    size_t cw0;                 // first codeword of the lane
-    bool live;
-};
-
-template <class C, bool ENC, int G, int I>
-__device__ __forceinline__ void flush(const Pending<C> &pd, const PsArgs &a, int lane) {
-    if (!pd.live) return;
-    if constexpr (ENC) {
-        // workspace [NR][ws_pitch]: syndrome-major, one byte per codeword (coalesced dwords)
-        uint8_t *dst = a.ws + pd.cw0;
-#pragma unroll
-        for (int qd = 0; qd < C::NQ; ++qd)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int si = C::SYN[G][I][qd][j];
-                if (si >= 0) *reinterpret_cast<uint32_t *>(dst + si * a.ws_pitch) = pd.D[qd][j];
-            }
-    } else {
-        if (G == 0 && I == 0) {   // one wave writes the results
-            if (pd.cw0 + 3 < a.ncw) {
-                *reinterpret_cast<int4 *>(a.result + pd.cw0) =
-                    make_int4(pd.res[0], pd.res[1], pd.res[2], pd.res[3]);
-            } else {
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if (pd.cw0 + k < a.ncw) a.result[pd.cw0 + k] = pd.res[k];
-            }
-        }
-        if (pd.flags) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (!(pd.flags >> k & 1)) continue;
-                uint8_t *dst = a.ws + (pd.cw0 + k) * 32;
-#pragma unroll
-                for (int qd = 0; qd < C::NQ; ++qd)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int si = C::SYN[G][I][qd][j];
-                        if (si >= 0) dst[si] = (uint8_t)(pd.D[qd][j] >> (8 * k));
-                    }
-            }
-        }
-    }
-    (void)lane;
-}
-
-template <class C, bool ENC, int G, int I>
-__device__ __forceinline__ void wave_body(const PsArgs &a, uint8_t *lds, uint32_t (*flags)[64],
-                                          int wave, int lane) {
-    constexpr int S = ENC ? C::S_ENC : C::S_DEC;
-    constexpr int NB = S / 8;
-    constexpr int q = 2 * (I & 1) + (I >> 1);              // slice (inverse of I = 2 (q&1) + (q>>1))
-    const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void *)a.base, (short)0, (int)a.span, 0x00020000);
-    // the lane's row starts relative to the tile image, shifted so that position p' of row k is
-    // at byte rb[k] + p' of the buffer
-    int rb[4];
-    uint32_t sh[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        rb[k] = kGuard + (4 * lane + k) * (int)a.stride - a.lo;
-        sh[k] = (uint32_t)rb[k] & 3u;
-    }
-    Pending<C> pd;
-    pd.live = false;
-    uint8_t *buf = lds;
-    uint32_t tile = blockIdx.x;
-    if (tile < a.ntiles) issue_tile(buf, a, rsrc, tile, wave, lane);
-    for (int it = 0; tile < a.ntiles; tile += gridDim.x, ++it) {
-        (void)it;
-        PS_STAMP(0);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();                                   // the tile has landed
-        PS_STAMP(1);
-        flush<C, ENC, G, I>(pd, a, lane);
-        if (tile == a.ntiles - 1) {
-            // A buffer load whose dword crosses the end of the range reads zero there: re-read the
-            // span's last bytes (the last row's tail) directly.
-            if (wave == 0) {
-                const uint32_t t0 = tile * a.stride * kTile;
-                const uint32_t tail = a.span - t0 < 64u ? a.span - t0 : 64u;
-                if ((uint32_t)lane < tail) {
-                    const uint32_t off = a.span - tail + lane;
-                    buf[kGuard + (off - t0)] = a.base[off];
-                }
-            }
-            __syncthreads();
-        }
-        const size_t cw0 = (size_t)tile * kTile + 4 * lane;
-        uint32_t ne = 0;
-        if (!ENC && a.neras) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (cw0 + k < a.ncw && a.neras[cw0 + k]) ne |= 1u << k;
-        }
-        uint32_t V[C::NLG][8];
-#pragma unroll
-        for (int s = 0; s < C::NLG; ++s)
-#pragma unroll
-            for (int t = 0; t < 8; ++t) V[s][t] = 0;
-        main_slice<C, G, NB>(V, buf, rb, sh, q * S, a.lo, a.hi);
-        if constexpr (q != 0) C::template fixup<G, S>(V, q);
-        PS_STAMP(2);
-        __syncthreads();                                   // every wave is done with the image
-        PS_STAMP(3);
-        uint32_t T[2][8];
-        reduce<C, q>(V, T, buf, wave, lane);
-        __syncthreads();                                   // the exchange area is read
-        // the next tile lands while this one's syndromes are folded (and the other workgroup on
-        // this CU computes)
-        if (tile + gridDim.x < a.ntiles) issue_tile(buf, a, rsrc, tile + gridDim.x, wave, lane);
-        PS_STAMP(4);
-        uint32_t Qd[C::NQ][8];
-        C::template epilogue<G, I>(T, Qd);
-        // quads -> bytes: after transpose8, Qd[qd][j] byte k = syndrome j of the quad, codeword k
-        uint32_t nz = 0;
-#pragma unroll
-        for (int qd = 0; qd < C::NQ; ++qd) {
-            uint32_t vm = 0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                if (C::SYN[G][I][qd][j] >= 0) vm |= 0x01010101u << j;
-#pragma unroll
-            for (int t = 0; t < 8; ++t) nz |= Qd[qd][t] & vm;
-            transpose8(Qd[qd]);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) pd.D[qd][j] = Qd[qd][j];
-        }
-        pd.cw0 = cw0;
-        pd.live = true;
-        PS_STAMP(5);
-        if constexpr (!ENC) {
-            uint32_t fl = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (nz >> (8 * k) & 0xFF) fl |= 1u << k;
-            flags[wave][lane] = fl;
-            __syncthreads();
-            fl = ne;
-#pragma unroll
-            for (int w = 0; w < kWaves; ++w) fl |= flags[w][lane];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (cw0 + k >= a.ncw) fl &= ~(1u << k);
-                pd.res[k] = (fl >> k & 1) ? kSentinel : 0;
-            }
-            pd.flags = fl;
-        }
-    }
-    flush<C, ENC, G, I>(pd, a, lane);
-}
-
-// Two workgroups per CU (16 waves, <= 128 VGPRs): while one waits for its tile or sits in a
-// barrier, the other computes.
-template <class C, bool ENC>
-__global__ void __launch_bounds__(kThreads, 4) k_ps_syndromes(PsArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kBufBytes];
-    __shared__ uint32_t flags[kWaves][64];
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    // wave (g, q): g = wave >> 2, q = wave & 3; epilogue index idx = 2 (q & 1) + (q >> 1)
-    switch (wave) {
-    case 0: wave_body<C, ENC, 0, 0>(a, lds, flags, wave, lane); break;
-    case 1: wave_body<C, ENC, 0, 2>(a, lds, flags, wave, lane); break;
-    case 2: wave_body<C, ENC, 0, 1>(a, lds, flags, wave, lane); break;
-    case 3: wave_body<C, ENC, 0, 3>(a, lds, flags, wave, lane); break;
-    case 4: wave_body<C, ENC, 1, 0>(a, lds, flags, wave, lane); break;
-    case 5: wave_body<C, ENC, 1, 2>(a, lds, flags, wave, lane); break;
-    case 6: wave_body<C, ENC, 1, 1>(a, lds, flags, wave, lane); break;
-    default: wave_body<C, ENC, 1, 3>(a, lds, flags, wave, lane); break;
-    }
 }
 
 // ---- helpers of the gather-layout kernels ------------------------------------------------------
@@ -710,291 +416,646 @@ k_py_syndromes(PsArgs a) {
     else py_body<C, ENC, 1>(a, buf, flags, lane);
 }
 
-// ---- group syndromes (default) -----------------------------------------------------------------
-// NW = 4 waves (one workgroup, 2 per CU) share a whole tile of 256 codewords (lane l: rows
-// l + 64k, byte k of its words) held in LDS in the swizzled gather layout of the pair kernel: two
-// 32 KiB halves (positions 0..127, 128..255), each 128-byte row chunk fetched by 8 lanes of one
-// LDS-DMA instruction.  Fetching both halves of every row together keeps each cache line read
-// once (windows fetched a half at a time re-read the lines the halves share from HBM once the
-// L2 no longer holds them: 3.5-4.4 TB/s vs 6.2-6.7 TB/s, tools/micro/py_dma.hip).  Wave q
-// evaluates ALL leaders over the 16-position pieces g = q, q + 4, q + 8, q + 12 with the PW blocks
-// of those positions (no fixups); two rounds of pairwise exchange through the consumed tile
-// buffer (recursive halving by owner bits: PG4_*::SEND / KEEP) leave each wave the totals of the
-// leaders it owns, whose syndromes it folds.  The next tile is fetched while the epilogues run
-// (and the other workgroup on the CU computes).
-constexpr int kPgTileBytes = 2 * kPyWinBytes;               // 64 KiB
+// Bytes s of a[0..3] -> one dword (a[0] in byte 0).
+__device__ __forceinline__ uint32_t gather4(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, int s) {
+    const uint32_t sel = (uint32_t)s | ((uint32_t)(s + 4) << 8) | 0x0c0c0000u;   // 0x0c: zero byte
+    const uint32_t x01 = __builtin_amdgcn_perm(a1, a0, sel), x23 = __builtin_amdgcn_perm(a3, a2, sel);
+    return __builtin_amdgcn_perm(x23, x01, 0x05040100u);
+}
 
-template <class C, bool ENC, int Q>
-__device__ __forceinline__ void pg_body(const PsArgs &a, uint8_t *buf, uint32_t (*flags)[64], int lane) {
-    constexpr int NW = C::NW, NL = C::NL, NLW = C::NLW;
-    constexpr int stamp_wave = Q;
-    (void)stamp_wave;
-    constexpr int NPW = 16 / NW;                                // pieces per wave
-    constexpr int IPW = 32 / NW;                                // DMA instructions per wave per half
-    constexpr int HI = ENC ? kN - C::NR : kN;                   // one past the last position
-    const int w_lo = a.lo / kPyWin;                             // first half holding positions >= lo
-    const pw_rsrc_t rsrc = pw_rsrc(a.base, a.span);
-    const uint32_t lbuf = __builtin_amdgcn_readfirstlane(lds_addr(buf));
-    auto fresh_lane = [&]() { uint32_t l = (uint32_t)lane; asm volatile("" : "+v"(l)); return l; };
-    // DMA: instruction i = 8k + m of a half covers rows 64k + 8m .. +7; lane j -> row 64k + 8m + j/8,
-    // piece (j & 7) ^ f(8m + j/8), f(l) = (l >> 1) & 7 (only depends on m & 1 and j/8)
-    auto doff = [&](uint32_t l, int k, int mp) {
-        const uint32_t dslot = l >> 3;
-        const uint32_t p = (l & 7) ^ ((4 * mp + (dslot >> 1)) & 7);
-        return (64 * k + dslot) * a.stride + 16 * p;
-    };
-    const uint32_t m_step = 8u * a.stride;
-    auto rd = [&](uint32_t l, int p) {                          // piece p of row 64k + l: + 8 KiB k
-        return 1024 * (l >> 3) + 128 * (l & 7) + 16 * (p ^ ((l >> 1) & 7));
-    };
-    const uint32_t tile_bytes = a.stride * kTile;
+// ---- tile kernel (default) ---------------------------------------------------------------------
+namespace pt {
 
-    auto issue = [&](uint32_t toff) {
-        if (a.ablate & 8) return;
-        const uint32_t l = fresh_lane();
-        for (int w = w_lo; w < 2; ++w) {                        // wave-uniform
-            const uint32_t base = toff + (uint32_t)(kPyWin * w - a.lo);
+constexpr int kThreads = 512;
+constexpr int kHalf = 32768;                  // one half image: 128 positions x 256 rows
+constexpr int kLds = 2 * kHalf + 16384;       // + exchange extension: 80 KiB, two workgroups per CU
+constexpr int kFlags = 2 * kHalf;             // decode flags [8][64] (extension, after the exchange)
+constexpr uint32_t kOob = 0xF0000000u;        // a buffer offset past every span (ps_max_rows)
+#ifndef EZRS_PT_PREFETCH
+#define EZRS_PT_PREFETCH 0
+#endif
+constexpr bool kPrefetch = EZRS_PT_PREFETCH;   // next piece's reads during the current one's 2nd block
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// The lane id, recomputed (v_mbcnt) wherever it is used: values derived from it are then not
+// hoisted out of the tile loop, where they would pin registers across the state.
+__device__ __forceinline__ uint32_t fresh(uint32_t = 0) {
+    uint32_t l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+// This lane's byte of piece p (0..7) of a half image, row block 0.
+__device__ __forceinline__ uint32_t piece_addr(uint32_t lbuf, uint32_t lane, int p) {
+    const uint32_t l = fresh(lane);
+    return lbuf + 1024u * (l >> 3) + 128u * (l & 7) + ((16u * p) ^ (16u * ((l >> 1) & 7)));
+}
+
+// LDS image of half h: piece p (16 positions) of row 64k + l at
+//   h kHalf + 8 KiB k + 1 KiB (l >> 3) + 128 (l & 7) + 16 (p ^ ((l >> 1) & 7)),
+// written by DMA instruction i = 8k + m (rows 64k + 8m .. +7, 1 KiB at h kHalf + i KiB): lane j
+// loads row 64k + 8m + j/8, piece (j & 7) ^ f(8m + j/8).  Wave w issues i = 4w .. 4w + 3.
+__device__ __forceinline__ void issue_half(uint32_t lbuf, pw_rsrc_t rsrc, uint32_t toff, int h, int lo,
+                                           uint32_t stride, int w, int ablate = 0) {
+    if (ablate & 8) return;
+    const uint32_t base = toff + 128u * h - (uint32_t)lo;
+    const uint32_t l = fresh();
+    const uint32_t dslot = l >> 3;
+    const uint32_t k = (uint32_t)w >> 1;
 #pragma unroll
-            for (int ii = 0; ii < IPW; ii += 2) {
-                const int i = Q * IPW + ii, k = i >> 3, m0 = i & 7;   // m0 even: (m0, m0 + 1)
-                const uint32_t d0 = base + doff(l, k, 0) + m0 * m_step, d1 = base + doff(l, k, 1) + (m0 + 1) * m_step;
-                asm volatile("s_mov_b32 m0, %0\n\t"
-                             "s_nop 0\n\t"
-                             "buffer_load_dwordx4 %1, %2, 0 offen lds"
-                             :: "s"(lbuf + w * kPyWinBytes + i * 1024), "v"(d0), "s"(rsrc) : "memory", "m0");
-                asm volatile("s_mov_b32 m0, %0\n\t"
-                             "s_nop 0\n\t"
-                             "buffer_load_dwordx4 %1, %2, 0 offen lds"
-                             :: "s"(lbuf + w * kPyWinBytes + (i + 1) * 1024), "v"(d1), "s"(rsrc) : "memory", "m0");
+    for (int ii = 0; ii < 4; ++ii) {
+        const uint32_t m = 4u * (w & 1) + ii;
+        const uint32_t p = (l & 7) ^ ((4u * (ii & 1) + (dslot >> 1)) & 7);
+        const uint32_t off = base + (64u * k + 8u * m + dslot) * stride + 16u * p;
+        asm volatile("s_mov_b32 m0, %0\n\t"
+                     "s_nop 0\n\t"
+                     "buffer_load_dwordx4 %1, %2, 0 offen lds"
+                     :: "s"(lbuf + h * kHalf + (8u * k + m) * 1024u), "v"(off), "s"(rsrc) : "memory", "m0");
+    }
+}
+
+__device__ __forceinline__ void read_piece(u32x4 (&R)[4], uint32_t addr) {
+    asm volatile("ds_read_b128 %0, %4\n\t"
+                 "ds_read_b128 %1, %4 offset:8192\n\t"
+                 "ds_read_b128 %2, %4 offset:16384\n\t"
+                 "ds_read_b128 %3, %4 offset:24576"
+                 : "=&v"(R[0]), "=&v"(R[1]), "=&v"(R[2]), "=&v"(R[3]) : "v"(addr) : "memory");
+}
+__device__ __forceinline__ void wait_piece(u32x4 (&R)[4]) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]) :: "memory");
+}
+template <int N> __device__ __forceinline__ void wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");
+}
+__device__ __forceinline__ void wait_lgkm() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+__device__ __forceinline__ void store_dword(pw_rsrc_t r, uint32_t off, uint32_t v) {
+    asm volatile("buffer_store_dword %0, %1, %2, 0 offen" :: "v"(v), "v"(off), "s"(r) : "memory");
+}
+__device__ __forceinline__ void store_byte(pw_rsrc_t r, uint32_t off, uint32_t v) {
+    asm volatile("buffer_store_byte %0, %1, %2, 0 offen" :: "v"(v), "v"(off), "s"(r) : "memory");
+}
+
+// Block b of piece I of group G's quarter-0 waves, applied at this wave's piece (quarter q): the
+// network of block B0 on positions pa .. pa+7, pa = 16 (p0 + q) + 8 b; positions >= HI (beyond
+// the codeword, or the parity positions when encoding) contribute nothing.
+template <class C, int G, int HI, int P0, int B>
+__device__ __forceinline__ void block8(uint32_t (&V)[C::NI][8], uint32_t (&X)[8], int q) {
+    constexpr int lo_pa = 16 * P0 + 8 * B;                        // quarter 0
+    constexpr int hi_pa = 16 * (P0 + C::QN - 1) + 8 * B;          // last quarter
+    if constexpr (lo_pa < HI) {
+        if constexpr (hi_pa + 8 > HI) {                           // some quarter reaches HI
+            const int d = HI - (16 * (P0 + q) + 8 * B);            // wave-uniform
+            if (d <= 0) return;
+            if (d < 8) {
+#pragma unroll
+                for (int t = 0; t < 8; ++t)
+                    if (t >= d) X[t] = 0;
             }
         }
-    };
-    // fix-ups of this wave's pieces (see pw_fix): straddling the span's ends, or before lo
-    auto fix = [&](uint32_t toff) {
-#pragma unroll 1
-        for (int i = 0; i < 4 * NPW; ++i) {
-            const int k = i & 3, g = Q + NW * (i >> 2), w = g >> 3, p = g & 7;
-            if (w < w_lo) continue;
-            const int64_t r0 = (int64_t)toff + (int64_t)(64 * k + lane) * a.stride;
-            const int64_t o = r0 + kPyWin * w + 16 * p - a.lo;
-            const bool straddle = (o < 0 && o > -16) || (o < (int64_t)a.span && o + 16 > (int64_t)a.span);
-            if (!straddle && o >= r0) continue;
-            const uint32_t dst = lbuf + w * kPyWinBytes + rd(lane, p) + 8192 * k;
-#pragma unroll 1
-            for (int j = 0; j < 16; ++j) {
-                const int64_t gg = o + j;
-                uint32_t v = 0;
-                if (gg >= r0 && !straddle) continue;
-                if (gg >= r0 && gg < (int64_t)a.span)
-                    asm volatile("global_load_ubyte %0, %1, off\n\ts_waitcnt vmcnt(0)"
-                                 : "=&v"(v) : "v"(a.base + gg) : "memory");
-                asm volatile("ds_write_b8 %0, %1\n\ts_waitcnt lgkmcnt(0)" :: "v"(dst + j), "v"(v) : "memory");
-            }
-        }
-    };
+        C::template block<G, 2 * P0 + B>(V, X);
+    }
+}
 
-    uint32_t pend[ENC ? C::NQW : 1][4];
-    size_t pend_cw0 = 0, pend_col = 0;
-    uint32_t pend_fl = 0;
-    bool pending = false;
-    auto flush = [&]() {
-        if (!pending || (a.ablate & 16)) return;
-        if constexpr (ENC) {
-            uint8_t *dst = a.ws + pend_col;
+// The pieces of half H of group G's waves at quarter q: quarter 0's pieces PIECE[G][I] + q.
+// Software-pipelined LDS reads when kPrefetch (the next piece's ds_reads in flight during the
+// current piece's second block).
+template <class C, int G, int H, int HI>
+__device__ __forceinline__ void half_pass(uint32_t (&V)[C::NI][8], uint32_t lbuf, int q) {
+    constexpr int I0 = H == 0 ? 0 : C::NP0[G];
+    constexpr int I1 = H == 0 ? C::NP0[G] : C::NP0[G] + C::NP1[G];
+    if constexpr (I1 > I0 && 16 * C::PIECE[G][I0] < HI) {
+        u32x4 R[4];
+        read_piece(R, piece_addr(lbuf + H * kHalf, 0, (C::PIECE[G][I0] + q) & 7));
+        static_for<I0, I1>([&](auto Ic) {
+            constexpr int I = decltype(Ic)::value;
+            constexpr int p0 = C::PIECE[G][I];
+            wait_piece(R);
+            uint32_t X[8];
+            {
+                const uint32_t c0[4] = {R[0].x, R[1].x, R[2].x, R[3].x};
+                const uint32_t c1[4] = {R[0].y, R[1].y, R[2].y, R[3].y};
+                transpose4x4(c0, X);
+                transpose4x4(c1, X + 4);
+            }
+            block8<C, G, HI, p0, 0>(V, X, q);
+            {
+                const uint32_t c2[4] = {R[0].z, R[1].z, R[2].z, R[3].z};
+                const uint32_t c3[4] = {R[0].w, R[1].w, R[2].w, R[3].w};
+                transpose4x4(c2, X);
+                transpose4x4(c3, X + 4);
+            }
+            if constexpr (I + 1 < I1 && kPrefetch) {
+                read_piece(R, piece_addr(lbuf + H * kHalf, 0, (C::PIECE[G][I + 1] + q) & 7));
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            block8<C, G, HI, p0, 1>(V, X, q);
+            if constexpr (I + 1 < I1 && !kPrefetch)
+                read_piece(R, piece_addr(lbuf + H * kHalf, 0, (C::PIECE[G][I + 1] + q) & 7));
+        });
+    }
+}
+
+// Positions before lo are the zero pad of a shortened code; the row windows fill them with the
+// previous row's bytes.  Each wave zeroes them in the pieces of half H it reads (every wave that
+// reads a piece writes the same bytes), after the half landed and before any read of it.
+template <class C, int G, int H>
+__device__ __forceinline__ void zero_pad(uint32_t lbuf, int q, int lo) {
+    constexpr int I0 = H == 0 ? 0 : C::NP0[G];
+    constexpr int I1 = H == 0 ? C::NP0[G] : C::NP0[G] + C::NP1[G];
+#pragma unroll 1
+    for (int i = I0; i < I1; ++i) {
+        const int pc = C::PIECE[G][i] + q;
+        const int n = lo - 16 * pc;                          // leading positions of the piece to clear
+        if (n <= 0) continue;                                // wave-uniform
+        const uint32_t at = piece_addr(lbuf + H * kHalf, 0, pc & 7);
+#pragma unroll 1
+        for (int k = 0; k < 4; ++k) {
+            u32x4 v = {0u, 0u, 0u, 0u};
+            if (n < 16) {
+                asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                             : "=&v"(v) : "v"(at + 8192u * k) : "memory");
 #pragma unroll
-            for (int qd = 0; qd < C::NQW; ++qd)
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) {
-                    const int si = C::SYN[Q][qd][jj];
-                    if (si >= 0) *reinterpret_cast<uint32_t *>(dst + (size_t)si * a.ws_pitch) = pend[qd][jj];
+                for (int d = 0; d < 4; ++d) {
+                    const int z = n - 4 * d;                 // bytes of dword d to clear
+                    const uint32_t m = z >= 4 ? 0u : z <= 0 ? ~0u : ~0u << (8 * z);
+                    v[d] &= m;
                 }
-        } else if (Q == 0) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (pend_cw0 + 64 * k < a.ncw) a.result[pend_cw0 + 64 * k] = (pend_fl >> k & 1) ? kSentinel : 0;
+            }
+            asm volatile("ds_write_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" :: "v"(at + 8192u * k), "v"(v) : "memory");
         }
-        pending = false;
-    };
+    }
+}
+
+// Pieces of half H that straddle the span's ends come back all-zero from the buffer load: re-read
+// their bytes one by one (first / last tile of a launch only; out-of-range bytes read as zero).
+// Every wave that reads a piece patches it itself, with the same bytes.  Offsets are 32-bit: a
+// "negative" offset (row 0 of a shortened code) wraps above every span.
+template <class C, int G, int H>
+__device__ __forceinline__ void fix_half(const PsArgs &a, pw_rsrc_t rsrc, uint32_t toff, uint32_t lbuf, int q) {
+    constexpr int I0 = H == 0 ? 0 : C::NP0[G];
+    constexpr int I1 = H == 0 ? C::NP0[G] : C::NP0[G] + C::NP1[G];
+#pragma unroll 1
+    for (int i = I0 * 4; i < I1 * 4; ++i) {
+        const int k = i & 3, p = (C::PIECE[G][i >> 2] + q) & 7;
+        const uint32_t o = toff + (64u * k + fresh()) * a.stride + 128u * H + 16u * p - (uint32_t)a.lo;
+        const bool straddle = o >= 0xFFFFFFF1u || (o < a.span && o + 16u > a.span);
+        if (!straddle) continue;
+        const uint32_t dst = piece_addr(lbuf + H * kHalf, 0, p) + 8192u * k;
+#pragma unroll 1
+        for (int j = 0; j < 16; ++j) {
+            uint32_t v;
+            asm volatile("buffer_load_ubyte %0, %1, %2, 0 offen\n\ts_waitcnt vmcnt(0)"
+                         : "=&v"(v) : "v"(o + j), "s"(rsrc) : "memory");
+            asm volatile("ds_write_b8 %0, %1\n\ts_waitcnt lgkmcnt(0)" :: "v"(dst + j), "v"(v) : "memory");
+        }
+    }
+}
+
+// One half of the tile for group G: fix-ups, then the pieces.
+template <class C, int G, int H, int HI>
+__device__ __forceinline__ void do_half(uint32_t (&V)[C::NI][8], const PsArgs &a, pw_rsrc_t rsrc,
+                                        uint32_t toff, uint32_t lbuf, int q, bool edge) {
+    if (__builtin_expect(edge, 0)) fix_half<C, G, H>(a, rsrc, toff, lbuf, q);
+    if (a.lo > 128 * H) zero_pad<C, G, H>(lbuf, q, a.lo);
+    half_pass<C, G, H, HI>(V, lbuf, q);
+}
+
+// Recursive-halving exchange, sub-rounds S.. (see gen_ps.py PtRole): send the XS items to the
+// area, then add the partner's XV items.  lx = this lane's byte in wave 0's slot 0.
+template <class C, int W, int S, int J = 0>
+__device__ __forceinline__ void xsend(uint32_t (&V)[C::NI][8], uint32_t lx) {
+    if constexpr (J < C::XCAP) {
+        constexpr int it = C::XS[W][S][J];
+        if constexpr (it >= 0) {
+            const u32x4 w0 = {V[it][0], V[it][1], V[it][2], V[it][3]};
+            const u32x4 w1 = {V[it][4], V[it][5], V[it][6], V[it][7]};
+            asm volatile("ds_write_b128 %0, %1 offset:%3\n\t"
+                         "ds_write_b128 %0, %2 offset:%4"
+                         :: "v"(lx), "v"(w0), "v"(w1), "n"((W * C::XCAP + J) * 2048),
+                            "n"((W * C::XCAP + J) * 2048 + 1024) : "memory");
+        }
+        xsend<C, W, S, J + 1>(V, lx);
+    }
+}
+template <class C, int W, int S, int J = 0>
+__device__ __forceinline__ void xrecv(uint32_t (&V)[C::NI][8], uint32_t lx) {
+    if constexpr (J < C::XCAP) {
+        constexpr int it = C::XV[W][S][J];
+        constexpr int PW = W ^ (C::GN << C::XR[S]);
+        if constexpr (it >= 0) {
+            u32x4 w0, w1;
+            asm volatile("ds_read_b128 %0, %2 offset:%3\n\t"
+                         "ds_read_b128 %1, %2 offset:%4\n\t"
+                         "s_waitcnt lgkmcnt(0)"
+                         : "=&v"(w0), "=&v"(w1) : "v"(lx), "n"((PW * C::XCAP + J) * 2048),
+                           "n"((PW * C::XCAP + J) * 2048 + 1024) : "memory");
+            V[it][0] ^= w0.x; V[it][1] ^= w0.y; V[it][2] ^= w0.z; V[it][3] ^= w0.w;
+            V[it][4] ^= w1.x; V[it][5] ^= w1.y; V[it][6] ^= w1.z; V[it][7] ^= w1.w;
+        }
+        xrecv<C, W, S, J + 1>(V, lx);
+    }
+}
+template <class C, int W, int S>
+__device__ __forceinline__ void exchange(uint32_t (&V)[C::NI][8], uint32_t lx) {
+    if constexpr (S < C::NSUB) {
+        xsend<C, W, S>(V, lx);
+        wait_lgkm();
+        barrier();
+        xrecv<C, W, S>(V, lx);
+        barrier();                                           // read before the area is reused
+        exchange<C, W, S + 1>(V, lx);
+    }
+}
+
+// Stores of one tile's epilogue, the same count for every wave so that every vmcnt is a
+// compile-time constant: decode, 4 results + one byte store per syndrome slot (4 x 4) and codeword
+// of the lane (flagged codewords only; the others and the empty slots go out of range); encode,
+// one dword per syndrome slot (the lane's 4 codewords' bytes, tile-lane column order).
+template <bool ENC> constexpr int n_stores() { return ENC ? 4 : 4 + 16; }
+
+// Fix-up, exchange, fold and stores of wave W (its own tables and epilogue).
+template <class C, bool ENC, int W>
+__device__ __forceinline__ void wave_tail(uint32_t (&V)[C::NI][8], const PsArgs &a, uint32_t lbuf, uint32_t tile,
+                                          uint32_t noff, pw_rsrc_t rsrc, pw_rsrc_t rout, pw_rsrc_t rws) {
+    constexpr int G = W % C::GN, Q = W / C::GN;
+    if (!(a.ablate & 2)) {
+        if constexpr (Q > 0) C::template fix<G, Q>(V);      // quarter 0's weights -> this quarter's
+        // exchange through the half-1 image + extension: wave W's slot j at (W XCAP + j) 2 KiB
+        exchange<C, W, 0>(V, lbuf + kHalf + 16u * fresh());
+    }
+    issue_half(lbuf, rsrc, noff, 1, a.lo, a.stride, W, a.ablate);    // the next tile's half 1
+    uint32_t T[C::NOWN][8];
+#pragma unroll
+    for (int i = 0; i < C::NOWN; ++i)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) T[i][t] = C::OWN[W][i] >= 0 ? V[C::OWN[W][i] < 0 ? 0 : C::OWN[W][i]][t] : 0u;
+    uint32_t Qs[8] = {0, 0, 0, 0, 0, 0, 0, 0}, nz = 0;
+    constexpr uint32_t vm = (C::SYN[W][0][0] >= 0 ? 0x01010101u : 0u) | (C::SYN[W][0][1] >= 0 ? 0x02020202u : 0u) |
+                            (C::SYN[W][0][2] >= 0 ? 0x04040404u : 0u) | (C::SYN[W][0][3] >= 0 ? 0x08080808u : 0u);
+    if (!(a.ablate & 4))
+        C::template epilogue<W>(T, [&](auto, uint32_t (&Qw)[8]) {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                nz |= Qw[t] & vm;
+                Qs[t] = Qw[t];
+            }
+        });
+    if constexpr (ENC) {
+        transpose8(Qs);                                      // Qs[jj] byte k: syndrome jj, codeword k
+        // column tile 256 + 4 l + k <-> codeword tile 256 + 64 k + l (k_ps_parity8<PERM>)
+        const uint32_t col = tile * kTile + 4u * fresh();
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+            store_dword(rws, C::SYN[W][0][jj] >= 0 ? (uint32_t)(C::SYN[W][0][jj] * a.ws_pitch) + col : kOob, Qs[jj]);
+    } else {
+        uint32_t fl = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (nz >> (8 * k) & 0xFF) fl |= 1u << k;
+        // OR over the 8 waves
+        const uint32_t fa = lbuf + kFlags + 256u * W + 4u * fresh();
+        asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" :: "v"(fa), "v"(fl) : "memory");
+        barrier();
+        {
+            uint32_t f[8];
+            const uint32_t fb = lbuf + kFlags + 4u * fresh();
+            asm volatile("ds_read_b32 %0, %8\n\t"
+                         "ds_read_b32 %1, %8 offset:256\n\t"
+                         "ds_read_b32 %2, %8 offset:512\n\t"
+                         "ds_read_b32 %3, %8 offset:768\n\t"
+                         "ds_read_b32 %4, %8 offset:1024\n\t"
+                         "ds_read_b32 %5, %8 offset:1280\n\t"
+                         "ds_read_b32 %6, %8 offset:1536\n\t"
+                         "ds_read_b32 %7, %8 offset:1792\n\t"
+                         "s_waitcnt lgkmcnt(0)"
+                         : "=&v"(f[0]), "=&v"(f[1]), "=&v"(f[2]), "=&v"(f[3]), "=&v"(f[4]),
+                           "=&v"(f[5]), "=&v"(f[6]), "=&v"(f[7]) : "v"(fb) : "memory");
+            fl = f[0] | f[1] | f[2] | f[3] | f[4] | f[5] | f[6] | f[7];
+            if (a.ablate & 32) fl = 0;                       // timing runs: keep the error path idle
+        }
+        const uint32_t cw0 = tile * kTile + fresh();         // byte k <-> codeword cw0 + 64k
+        // results: wave 0 writes them, every other wave issues the same stores out of range
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            store_dword(rout, W == 0 ? (cw0 + 64u * k) * 4u : kOob, (fl >> k & 1) ? (uint32_t)kSentinel : 0u);
+        if (__ballot(fl != 0) != 0) transpose8(Qs);          // Qs[jj] byte k: syndrome jj, codeword k
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t row = (fl >> k & 1) ? (cw0 + 64u * k) * 32u : kOob;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj)
+                store_byte(rws, C::SYN[W][0][jj] >= 0 ? row + C::SYN[W][0][jj] : kOob, Qs[jj] >> (8 * k));
+        }
+    }
+}
+
+// The tile loop of the waves of leader group G (wave w = G + GN q): one copy of the main loop per
+// group; the per-wave tails differ.
+template <class C, bool ENC, int G>
+__device__ __forceinline__ void pt_run(const PsArgs &a, uint8_t *lds, int w) {
+    constexpr int HI = ENC ? kN - (int)C::NR : kN;            // positions evaluated
+    constexpr int NST = n_stores<ENC>();
+    const int q = w / C::GN;
+    const pw_rsrc_t rsrc = pw_rsrc(a.base, a.span);
+    const uint32_t lbuf = __builtin_amdgcn_readfirstlane(lds_addr(lds));
+    const uint32_t tile_bytes = a.stride * kTile;
+    const pw_rsrc_t rout = pw_rsrc(reinterpret_cast<const uint8_t *>(a.result), ENC ? 0u : a.ncw * 4u);
+    // decode: [ncw][32] flagged syndromes; encode: [NR][ws_pitch] syndrome-major, tile-lane order
+    const pw_rsrc_t rws = pw_rsrc(a.ws, ENC ? (uint32_t)(C::NR * a.ws_pitch) : a.ncw * 32u);
 
     uint32_t tile = blockIdx.x;
-    if (tile < a.ntiles) issue(tile * tile_bytes);
+    issue_half(lbuf, rsrc, tile * tile_bytes, 0, a.lo, a.stride, w, a.ablate);
+    issue_half(lbuf, rsrc, tile * tile_bytes, 1, a.lo, a.stride, w, a.ablate);
     for (int it = 0; tile < a.ntiles; tile += gridDim.x, ++it) {
-        (void)it;
-        PG_STAMP(0);
         const uint32_t toff = tile * tile_bytes;
-        uint32_t V[NL][8];
+        const bool more = tile + gridDim.x < a.ntiles;
+        const uint32_t noff = more ? toff + gridDim.x * tile_bytes : kOob;
+        const bool edge = (tile == 0 && (a.lo & 15)) || toff + tile_bytes + 256u > a.span;
+        uint32_t V[C::NI][8];
 #pragma unroll
-        for (int s = 0; s < NL; ++s)
+        for (int s = 0; s < C::NI; ++s)
 #pragma unroll
             for (int t = 0; t < 8; ++t) V[s][t] = 0;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        PG_STAMP(1);
-        __syncthreads();                                         // the tile landed (all waves)
-        PG_STAMP(2);
-        flush();
-        if (__builtin_expect(a.lo > 0 || (int64_t)toff + tile_bytes + kPyWin > (int64_t)a.span, 0)) fix(toff);
-        if (!(a.ablate & 1)) static_for<0, NPW>([&](auto Jc) {
-            constexpr int g = Q + NW * decltype(Jc)::value, w = g >> 3, p = g & 7;
-            constexpr int p16 = kPyWin * w + 16 * p;             // first position of the piece
-            if constexpr (p16 < HI) {
-                if (w < w_lo) return;                            // wave-uniform (shortened codes)
-                uint4 R[4];
-                asm volatile("ds_read_b128 %0, %4\n\t"
-                             "ds_read_b128 %1, %4 offset:8192\n\t"
-                             "ds_read_b128 %2, %4 offset:16384\n\t"
-                             "ds_read_b128 %3, %4 offset:24576\n\t"
-                             "s_waitcnt lgkmcnt(0)"
-                             : "=&v"(R[0]), "=&v"(R[1]), "=&v"(R[2]), "=&v"(R[3])
-                             : "v"(lbuf + w * kPyWinBytes + rd(fresh_lane(), p)) : "memory");
-                uint32_t X[16];
+        // half 0 landed (younger: this tile's half 1, the previous tile's stores)
+        if (it) wait_vm<4 + NST>(); else wait_vm<4>();
+        barrier();
+        if (!(a.ablate & 1)) do_half<C, G, 0, HI>(V, a, rsrc, toff, lbuf, q, edge);
+        barrier();                                           // half 0 consumed
+        issue_half(lbuf, rsrc, noff, 0, a.lo, a.stride, w, a.ablate);  // the next tile's half 0
+        // half 1 landed (younger: the previous tile's stores, the next tile's half 0)
+        if (it) wait_vm<4 + NST>(); else wait_vm<4>();
+        barrier();
+        if (!(a.ablate & 1)) do_half<C, G, 1, HI>(V, a, rsrc, toff, lbuf, q, edge);
+        barrier();                                           // half 1 consumed
+        static_assert(C::QN <= 8, "");
+        switch (q) {
+        case 0: wave_tail<C, ENC, G>(V, a, lbuf, tile, noff, rsrc, rout, rws); break;
+        case 1: if constexpr (C::QN > 1) wave_tail<C, ENC, G + C::GN>(V, a, lbuf, tile, noff, rsrc, rout, rws); break;
+        case 2: if constexpr (C::QN > 2) wave_tail<C, ENC, G + 2 * C::GN>(V, a, lbuf, tile, noff, rsrc, rout, rws); break;
+        case 3: if constexpr (C::QN > 3) wave_tail<C, ENC, G + 3 * C::GN>(V, a, lbuf, tile, noff, rsrc, rout, rws); break;
+        case 4: if constexpr (C::QN > 4) wave_tail<C, ENC, G + 4 * C::GN>(V, a, lbuf, tile, noff, rsrc, rout, rws); break;
+        case 5: if constexpr (C::QN > 5) wave_tail<C, ENC, G + 5 * C::GN>(V, a, lbuf, tile, noff, rsrc, rout, rws); break;
+        case 6: if constexpr (C::QN > 6) wave_tail<C, ENC, G + 6 * C::GN>(V, a, lbuf, tile, noff, rsrc, rout, rws); break;
+        default: if constexpr (C::QN > 7) wave_tail<C, ENC, G + 7 * C::GN>(V, a, lbuf, tile, noff, rsrc, rout, rws); break;
+        }
+    }
+    wait_vm<0>();                                            // no DMA may land after the exit
+}
+
+// ---- linear variant (odd row pitch): the whole tile by linear 1 KiB LDS-DMA ----------------------
+// The tile's rows are one contiguous span; 64 line-aligned 1 KiB DMA instructions copy it to LDS as
+// it lies (fetch-efficient: every 128-byte line is read once, by one instruction).  Lane l owns rows
+// 4l .. 4l+3 (byte k of its words = row 4l + k): with an odd pitch P the rows' starts 4lP fall in
+// 32 distinct LDS banks, so the row reads (ds_read2_b32, 4-byte aligned, then v_alignbyte by the
+// row's byte phase (kP - lo) mod 4) are conflict-free.  One tile buffer per workgroup; the other
+// workgroup on the CU computes while this one's next tile lands.
+constexpr int kGuard = 256;                      // bytes before the image: row 0's pad positions
+constexpr int kLinFlags = kGuard + 65536 + 64;   // decode flags [8][64] after the image
+static_assert(kLinFlags + 2048 <= kLds, "linear variant LDS");
+
+__device__ __forceinline__ void issue_tile_lin(uint32_t lbuf, pw_rsrc_t rsrc, uint32_t toff, uint32_t tile_bytes,
+                                               int w, int ablate) {
+    if (ablate & 8) return;
+    const uint32_t ninstr = (tile_bytes + 1023) >> 10;
+    const uint32_t lo16 = 16u * fresh();
+    for (uint32_t i = w; i < ninstr; i += 8)
+        asm volatile("s_mov_b32 m0, %0\n\t"
+                     "s_nop 0\n\t"
+                     "buffer_load_dwordx4 %1, %2, 0 offen lds"
+                     :: "s"(lbuf + kGuard + i * 1024u), "v"(toff + i * 1024u + lo16), "s"(rsrc) : "memory", "m0");
+}
+
+// Positions pa .. pa+7 (words X) with the network of quarter 0's block B0; positions before lo
+// (the zero pad of a shortened code: the image holds the previous row's bytes there) and at or
+// past HI contribute nothing.  pa, lo wave-uniform.
+template <class C, int G, int HI, int B0>
+__device__ __forceinline__ void block8_rt(uint32_t (&V)[C::NI][8], uint32_t (&X)[8], int pa, int lo) {
+    const int dlo = lo - pa, dhi = HI - pa;
+    if (dhi <= 0 || dlo >= 8) return;
+    if (dlo > 0 || dhi < 8) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+            if (t < dlo || t >= dhi) X[t] = 0;
+    }
+    C::template block<G, B0>(V, X);
+}
+
+// Rows 4l + k, positions pa .. pa+15 (k = 0..3): R[k] = 16 bytes of row k.
+__device__ __forceinline__ void read_rows_lin(u32x4 (&R)[4], uint32_t lbuf, uint32_t stride, int pa, int lo,
+                                              const uint32_t (&ph)[4]) {
+    const uint32_t base = lbuf + kGuard + 4u * fresh() * stride + (uint32_t)(pa - lo);
+    u32x2 e[4][2];
+    uint32_t d4[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t at = (base + k * stride) & ~3u;
+        asm volatile("ds_read2_b32 %0, %3 offset1:1\n\t"
+                     "ds_read2_b32 %1, %3 offset0:2 offset1:3\n\t"
+                     "ds_read_b32 %2, %3 offset:16"
+                     : "=&v"(e[k][0]), "=&v"(e[k][1]), "=&v"(d4[k]) : "v"(at) : "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(e[0][0]), "+v"(e[0][1]), "+v"(d4[0]), "+v"(e[1][0]), "+v"(e[1][1]), "+v"(d4[1]),
+                   "+v"(e[2][0]), "+v"(e[2][1]), "+v"(d4[2]), "+v"(e[3][0]), "+v"(e[3][1]), "+v"(d4[3])
+                 :: "memory");
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t d[5] = {e[k][0].x, e[k][0].y, e[k][1].x, e[k][1].y, d4[k]};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) R[k][j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], ph[k]);
+    }
+}
+
+template <class C, int G, int HI>
+__device__ __forceinline__ void lin_pass(uint32_t (&V)[C::NI][8], uint32_t lbuf, uint32_t stride, int q, int lo,
+                                         const uint32_t (&ph)[4]) {
+    constexpr int NP = C::NP0[G] + C::NP1[G];
+    static_for<0, NP>([&](auto Ic) {
+        constexpr int I = decltype(Ic)::value;
+        constexpr int p0 = C::PIECE[G][I];
+        if constexpr (16 * p0 < HI) {
+            const int pa = 16 * (p0 + q);
+            if (pa < HI) {                                   // wave-uniform
+                u32x4 R[4];
+                read_rows_lin(R, lbuf, stride, pa, lo, ph);
+                uint32_t X[8];
                 {
                     const uint32_t c0[4] = {R[0].x, R[1].x, R[2].x, R[3].x};
                     const uint32_t c1[4] = {R[0].y, R[1].y, R[2].y, R[3].y};
-                    const uint32_t c2[4] = {R[0].z, R[1].z, R[2].z, R[3].z};
-                    const uint32_t c3[4] = {R[0].w, R[1].w, R[2].w, R[3].w};
                     transpose4x4(c0, X);
                     transpose4x4(c1, X + 4);
-                    transpose4x4(c2, X + 8);
-                    transpose4x4(c3, X + 12);
                 }
-                static_for<0, 2>([&](auto Bc) {
-                    constexpr int p0 = p16 + 8 * decltype(Bc)::value;
-                    if constexpr (p0 < HI) {
-                        uint32_t Y[8];
+                block8_rt<C, G, HI, 2 * p0>(V, X, pa, lo);
+                {
+                    const uint32_t c2[4] = {R[0].z, R[1].z, R[2].z, R[3].z};
+                    const uint32_t c3[4] = {R[0].w, R[1].w, R[2].w, R[3].w};
+                    transpose4x4(c2, X);
+                    transpose4x4(c3, X + 4);
+                }
+                block8_rt<C, G, HI, 2 * p0 + 1>(V, X, pa + 8, lo);
+            }
+        }
+    });
+}
+
+// Fix-up, exchange (through the consumed image), next tile's DMA, fold and stores of wave W.
+template <class C, bool ENC, int W>
+__device__ __forceinline__ void wave_tail_lin(uint32_t (&V)[C::NI][8], const PsArgs &a, uint32_t lbuf,
+                                              uint32_t tile, uint32_t noff, uint32_t tile_bytes,
+                                              pw_rsrc_t rsrc, pw_rsrc_t rout, pw_rsrc_t rws) {
+    constexpr int G = W % C::GN, Q = W / C::GN;
+    if (!(a.ablate & 2)) {
+        if constexpr (Q > 0) C::template fix<G, Q>(V);      // quarter 0's weights -> this quarter's
+        exchange<C, W, 0>(V, lbuf + kGuard + 16u * fresh());
+    }
+    if (noff != kOob) issue_tile_lin(lbuf, rsrc, noff, tile_bytes, W, a.ablate);
+    uint32_t T[C::NOWN][8];
 #pragma unroll
-                        for (int t = 0; t < 8; ++t) Y[t] = p0 + t < HI ? X[p0 - p16 + t] : 0u;
-                        C::template block<p0 / 8>(V, Y);
-                    }
-                });
+    for (int i = 0; i < C::NOWN; ++i)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) T[i][t] = C::OWN[W][i] >= 0 ? V[C::OWN[W][i] < 0 ? 0 : C::OWN[W][i]][t] : 0u;
+    uint32_t Qs[8] = {0, 0, 0, 0, 0, 0, 0, 0}, nz = 0;
+    constexpr uint32_t vm = (C::SYN[W][0][0] >= 0 ? 0x01010101u : 0u) | (C::SYN[W][0][1] >= 0 ? 0x02020202u : 0u) |
+                            (C::SYN[W][0][2] >= 0 ? 0x04040404u : 0u) | (C::SYN[W][0][3] >= 0 ? 0x08080808u : 0u);
+    if (!(a.ablate & 4))
+        C::template epilogue<W>(T, [&](auto, uint32_t (&Qw)[8]) {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                nz |= Qw[t] & vm;
+                Qs[t] = Qw[t];
             }
         });
-        PG_STAMP(3);
-        __syncthreads();                                         // every wave is done with the tile
-        PG_STAMP(4);
-        // recursive-halving exchange through the tile buffer
-        if (!(a.ablate & 2)) static_for<0, C::ROUNDS>([&](auto Rc) {
-            constexpr int r = decltype(Rc)::value, P = Q ^ (1 << r), NS = C::NSEND[r];
-            uint4 *x = reinterpret_cast<uint4 *>(buf);
+    const uint32_t cw0 = tile * kTile + 4u * fresh();        // byte k <-> codeword cw0 + k
+    if constexpr (ENC) {
+        transpose8(Qs);                                      // Qs[jj] byte k: syndrome jj, codeword k
+        // syndrome-major workspace in codeword order: the dword at column cw0 holds cw0 .. cw0+3
 #pragma unroll
-            for (int i = 0; i < NS; ++i) {
-                const int s = C::SEND[Q][r][i];
-                if (s < 0) continue;
+        for (int jj = 0; jj < 4; ++jj)
+            if (C::SYN[W][0][jj] >= 0) store_dword(rws, (uint32_t)(C::SYN[W][0][jj] * a.ws_pitch) + cw0, Qs[jj]);
+    } else {
+        uint32_t fl = 0;
 #pragma unroll
-                for (int h = 0; h < 2; ++h)
-                    x[((Q * NS + i) * 2 + h) * 64 + lane] =
-                        make_uint4(V[s][4 * h], V[s][4 * h + 1], V[s][4 * h + 2], V[s][4 * h + 3]);
-            }
-            __syncthreads();
+        for (int k = 0; k < 4; ++k)
+            if (nz >> (8 * k) & 0xFF) fl |= 1u << k;
+        const uint32_t fa = lbuf + kLinFlags + 256u * W + 4u * fresh();
+        asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" :: "v"(fa), "v"(fl) : "memory");
+        barrier();
+        {
+            uint32_t f[8];
+            const uint32_t fb = lbuf + kLinFlags + 4u * fresh();
+            asm volatile("ds_read_b32 %0, %8\n\t"
+                         "ds_read_b32 %1, %8 offset:256\n\t"
+                         "ds_read_b32 %2, %8 offset:512\n\t"
+                         "ds_read_b32 %3, %8 offset:768\n\t"
+                         "ds_read_b32 %4, %8 offset:1024\n\t"
+                         "ds_read_b32 %5, %8 offset:1280\n\t"
+                         "ds_read_b32 %6, %8 offset:1536\n\t"
+                         "ds_read_b32 %7, %8 offset:1792\n\t"
+                         "s_waitcnt lgkmcnt(0)"
+                         : "=&v"(f[0]), "=&v"(f[1]), "=&v"(f[2]), "=&v"(f[3]), "=&v"(f[4]),
+                           "=&v"(f[5]), "=&v"(f[6]), "=&v"(f[7]) : "v"(fb) : "memory");
+            fl = f[0] | f[1] | f[2] | f[3] | f[4] | f[5] | f[6] | f[7];
+            if (a.ablate & 32) fl = 0;                       // timing runs: keep the error path idle
+        }
+        if constexpr (W == 0) {
 #pragma unroll
-            for (int i = 0; i < NS; ++i) {
-                const int s = C::KEEP[Q][r][i];
-                if (s < 0) continue;
+            for (int k = 0; k < 4; ++k)
+                store_dword(rout, (cw0 + k) * 4u, (fl >> k & 1) ? (uint32_t)kSentinel : 0u);
+        }
+        if (__ballot(fl != 0) != 0) {                        // flagged codewords: their syndromes
+            transpose8(Qs);                                  // Qs[jj] byte k: syndrome jj, codeword k
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const uint4 v = x[((P * NS + i) * 2 + h) * 64 + lane];
-                    V[s][4 * h] ^= v.x;
-                    V[s][4 * h + 1] ^= v.y;
-                    V[s][4 * h + 2] ^= v.z;
-                    V[s][4 * h + 3] ^= v.w;
-                }
-            }
-            __syncthreads();                                     // read before reuse / the next DMA
-        });
-        PG_STAMP(5);
-        if (tile + gridDim.x < a.ntiles) issue(toff + gridDim.x * tile_bytes);
-        uint32_t T[NLW][8];
-#pragma unroll
-        for (int i = 0; i < NLW; ++i)
-#pragma unroll
-            for (int t = 0; t < 8; ++t) T[i][t] = C::OWN[Q][i] >= 0 ? V[C::OWN[Q][i] < 0 ? 0 : C::OWN[Q][i]][t] : 0u;
-        const size_t cw0 = (size_t)tile * kTile + lane;          // byte k <-> codeword cw0 + 64k
-        uint32_t nz = 0;
-        uint32_t D[C::NQW][4];
-#pragma unroll
-        for (int qd = 0; qd < C::NQW; ++qd)
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj) D[qd][jj] = T[0][jj + qd];
-        if (!(a.ablate & 4)) C::template epilogue<Q>(T, [&](auto Qc, uint32_t (&Qw)[8]) {
-            constexpr int qd = decltype(Qc)::value;
-            if constexpr (!ENC) {
-                uint32_t vm = 0;
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t row = (fl >> k & 1) ? (cw0 + k) * 32u : kOob;
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj)
-                    if (C::SYN[Q][qd][jj] >= 0) vm |= 0x01010101u << jj;
-#pragma unroll
-                for (int t = 0; t < 8; ++t) nz |= Qw[t] & vm;
-            }
-            transpose8(Qw);
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj) D[qd][jj] = Qw[jj];
-        });
-        pend_cw0 = cw0;
-        pend_col = (size_t)tile * kTile + 4 * lane;
-        pending = true;
-        PG_STAMP(6);
-        if constexpr (ENC) {
-#pragma unroll
-            for (int qd = 0; qd < C::NQW; ++qd)
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) pend[qd][jj] = D[qd][jj];
-        } else {
-            uint32_t fl = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (nz >> (8 * k) & 0xFF) fl |= 1u << k;
-            // OR over the waves (asm: the compiler would wait for the DMA in flight)
-            const uint32_t fa = lds_addr(reinterpret_cast<uint8_t *>(&flags[Q][lane]));
-            asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" :: "v"(fa), "v"(fl) : "memory");
-            __syncthreads();
-#pragma unroll
-            for (int q = 0; q < NW; ++q) {
-                if (q == Q) continue;
-                const uint32_t fb = lds_addr(reinterpret_cast<uint8_t *>(&flags[q][lane]));
-                uint32_t fo;
-                asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(fo) : "v"(fb) : "memory");
-                fl |= fo;
-            }
-            if (a.neras) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if (cw0 + 64 * k < a.ncw && a.neras[cw0 + 64 * k]) fl |= 1u << k;
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (cw0 + 64 * k >= a.ncw) fl &= ~(1u << k);
-            pend_fl = fl;
-            if (fl) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    if (!(fl >> k & 1)) continue;
-                    uint8_t *dst = a.ws + (cw0 + 64 * k) * 32;
-#pragma unroll
-                    for (int qd = 0; qd < C::NQW; ++qd)
-#pragma unroll
-                        for (int jj = 0; jj < 4; ++jj) {
-                            const int si = C::SYN[Q][qd][jj];
-                            if (si >= 0) dst[si] = (uint8_t)(D[qd][jj] >> (8 * k));
-                        }
-                }
+                    if (C::SYN[W][0][jj] >= 0) store_byte(rws, row + C::SYN[W][0][jj], Qs[jj] >> (8 * k));
             }
         }
     }
-    flush();
+}
+
+template <class C, bool ENC, int G>
+__device__ __forceinline__ void pt_run_lin(const PsArgs &a, uint8_t *lds, int w) {
+    constexpr int HI = ENC ? kN - (int)C::NR : kN;
+    const pw_rsrc_t rsrc = pw_rsrc(a.base, a.span);
+    const uint32_t lbuf = __builtin_amdgcn_readfirstlane(lds_addr(lds));
+    const uint32_t tile_bytes = a.stride * kTile;
+    const pw_rsrc_t rout = pw_rsrc(reinterpret_cast<const uint8_t *>(a.result), ENC ? 0u : a.ncw * 4u);
+    const pw_rsrc_t rws = pw_rsrc(a.ws, ENC ? (uint32_t)(C::NR * a.ws_pitch) : a.ncw * 32u);
+    uint32_t tile = blockIdx.x;
+    issue_tile_lin(lbuf, rsrc, tile * tile_bytes, tile_bytes, w, a.ablate);
+    for (; tile < a.ntiles; tile += gridDim.x) {
+        // run-time values re-read each tile: nothing derived from them is hoisted out of the loop
+        int q = w / C::GN, lo = a.lo;
+        asm volatile("" : "+s"(q), "+s"(lo));
+        uint32_t ph[4];                                      // byte phase of row k's start
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ph[k] = (lbuf + kGuard + k * a.stride - (uint32_t)lo) & 3u;
+        const uint32_t toff = tile * tile_bytes;
+        const uint32_t noff = tile + gridDim.x < a.ntiles ? toff + gridDim.x * tile_bytes : kOob;
+        uint32_t V[C::NI][8];
+#pragma unroll
+        for (int s = 0; s < C::NI; ++s)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) V[s][t] = 0;
+        wait_vm<0>();                                        // the tile landed (and the stores went)
+        barrier();
+        if (toff + tile_bytes > a.span) {                    // last tile: the span's final bytes
+            // a 16-byte DMA piece that crosses the span's end comes back all-zero: re-read the last
+            // 64 bytes one by one (out-of-range bytes read as zero)
+            if (w == 0) {
+                const uint32_t off = a.span - 64u + fresh();
+                uint32_t v;
+                asm volatile("buffer_load_ubyte %0, %1, %2, 0 offen\n\ts_waitcnt vmcnt(0)"
+                             : "=&v"(v) : "v"(off), "s"(rsrc) : "memory");
+                if (off >= toff && off < a.span)
+                    asm volatile("ds_write_b8 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                                 :: "v"(lbuf + kGuard + (off - toff)), "v"(v) : "memory");
+            }
+            barrier();
+        }
+        if (!(a.ablate & 1)) lin_pass<C, G, HI>(V, lbuf, a.stride, q, lo, ph);
+        barrier();                                           // the image is consumed
+        switch (w / C::GN) {
+        case 0: wave_tail_lin<C, ENC, G>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws); break;
+        case 1: if constexpr (C::QN > 1) wave_tail_lin<C, ENC, G + C::GN>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws); break;
+        case 2: if constexpr (C::QN > 2) wave_tail_lin<C, ENC, G + 2 * C::GN>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws); break;
+        case 3: if constexpr (C::QN > 3) wave_tail_lin<C, ENC, G + 3 * C::GN>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws); break;
+        case 4: if constexpr (C::QN > 4) wave_tail_lin<C, ENC, G + 4 * C::GN>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws); break;
+        case 5: if constexpr (C::QN > 5) wave_tail_lin<C, ENC, G + 5 * C::GN>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws); break;
+        case 6: if constexpr (C::QN > 6) wave_tail_lin<C, ENC, G + 6 * C::GN>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws); break;
+        default: if constexpr (C::QN > 7) wave_tail_lin<C, ENC, G + 7 * C::GN>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws); break;
+        }
+    }
+    wait_vm<0>();                                            // no DMA may land after the exit
 }
 
 template <class C, bool ENC>
-__global__ void __attribute__((amdgpu_flat_work_group_size(256, 256), amdgpu_waves_per_eu(2)))
-k_pg_syndromes(PsArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t buf[kPgTileBytes];
-    __shared__ uint32_t flags[4][64];
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    switch (wave) {
-    case 0: pg_body<C, ENC, 0>(a, buf, flags, lane); break;
-    case 1: pg_body<C, ENC, 1>(a, buf, flags, lane); break;
-    case 2: pg_body<C, ENC, 2>(a, buf, flags, lane); break;
-    default: pg_body<C, ENC, 3>(a, buf, flags, lane); break;
-    }
+__global__ void __attribute__((amdgpu_flat_work_group_size(kThreads, kThreads), amdgpu_waves_per_eu(4)))
+k_pt_lin(PsArgs a) {
+    static_assert(C::NQ == 1, "one quad (4 syndromes) per wave");
+    static_assert(C::GN <= 2 && C::GN * C::QN == 8, "8 waves: at most two leader groups");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kLds];
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (C::GN == 1 || w % C::GN == 0) pt_run_lin<C, ENC, 0>(a, lds, w);
+    else pt_run_lin<C, ENC, C::GN - 1>(a, lds, w);
 }
+
+template <class C, bool ENC>
+__global__ void __attribute__((amdgpu_flat_work_group_size(kThreads, kThreads), amdgpu_waves_per_eu(4)))
+k_pt(PsArgs a) {
+    static_assert(C::NQ == 1, "one quad (4 syndromes) per wave");
+    static_assert(C::GN <= 2 && C::GN * C::QN == 8, "8 waves: at most two leader groups");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kLds];
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (C::GN == 1 || w % C::GN == 0) pt_run<C, ENC, 0>(a, lds, w);
+    else pt_run<C, ENC, C::GN - 1>(a, lds, w);
+}
+
+} // namespace pt
 
 // ---- encode, stage 2: parity = V^-1 S on 32-codeword bit-sliced registers -------------------
 // Syndromes (encode workspace) -> parity rows.
@@ -1007,93 +1068,6 @@ k_pg_syndromes(PsArgs a) {
 // padded by 8 bytes: conflict-free 8-byte stores); then the rows are stored.
 constexpr int kParGroups = 64;
 constexpr int kParCw = 32 * kParGroups;
-
-// Bytes s of a[0..3] -> one dword (a[0] in byte 0).
-__device__ __forceinline__ uint32_t gather4(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, int s) {
-    const uint32_t sel = (uint32_t)s | ((uint32_t)(s + 4) << 8) | 0x0c0c0000u;   // 0x0c: zero byte
-    const uint32_t x01 = __builtin_amdgcn_perm(a1, a0, sel), x23 = __builtin_amdgcn_perm(a3, a2, sel);
-    return __builtin_amdgcn_perm(x23, x01, 0x05040100u);
-}
-
-template <class C, bool PERM>
-__global__ void __launch_bounds__(256) k_ps_parity(const uint8_t *ws, size_t ws_pitch, uint8_t *parity,
-                                                   size_t pstride, size_t ncw) {
-    constexpr int NR = C::NR;
-    constexpr int kRegion = 32 * NR + 8;                       // bytes per group in the stage
-    constexpr int kPlanes = 8 * NR * kParGroups;               // dwords
-    constexpr int kStage = kParGroups * kRegion / 4;           // dwords
-    constexpr int kLds = kPlanes > kStage ? kPlanes : kStage;
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kLds];
-    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const size_t g0 = (size_t)blockIdx.x * kParGroups;
-    const uint8_t *src = ws + (g0 + lane) * 32;                // ws rows are padded to 2048 cw
-    for (int i = wave; i < NR; i += 4) {
-        const uint4 v0 = *reinterpret_cast<const uint4 *>(src + i * ws_pitch);
-        const uint4 v1 = *reinterpret_cast<const uint4 *>(src + i * ws_pitch + 16);
-        uint32_t D[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-        transpose8(D);                                         // D[q] bit 8k + m: cw 4m + k
-#pragma unroll
-        for (int qq = 0; qq < 8; ++qq) lds[(8 * i + qq) * 64 + lane] = D[qq];
-    }
-    __syncthreads();
-    uint32_t O[8][8];
-    switch (wave) {
-    case 0: C::template q_pass<0>(O, lds + lane, 64); break;
-    case 1: if constexpr (C::NPASS > 1) C::template q_pass<1>(O, lds + lane, 64); break;
-    case 2: if constexpr (C::NPASS > 2) C::template q_pass<2>(O, lds + lane, 64); break;
-    default: if constexpr (C::NPASS > 3) C::template q_pass<3>(O, lds + lane, 64); break;
-    }
-    __syncthreads();                                           // planes consumed
-    uint8_t *stage = reinterpret_cast<uint8_t *>(lds);
-    if (wave < C::NPASS) {
-        const int nj = NR - 8 * wave < 8 ? NR - 8 * wave : 8;
-#pragma unroll
-        for (int jl = 0; jl < 8; ++jl)
-            if (jl < nj) transpose8(O[jl]);                    // O[jl][m] byte k: symbol of cw 4m+k
-        uint8_t *reg = stage + lane * kRegion + 8 * wave;
-#pragma unroll
-        for (int m = 0; m < 8; ++m)
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                uint8_t *row = reg + (4 * m + k) * NR;
-                const uint32_t lo = gather4(O[0][m], O[1][m], O[2][m], O[3][m], k);
-                if (nj == 8) {
-                    const uint32_t hi = gather4(O[4][m], O[5][m], O[6][m], O[7][m], k);
-                    *reinterpret_cast<uint2 *>(row) = make_uint2(lo, hi);
-                } else if (nj == 4) {
-                    *reinterpret_cast<uint32_t *>(row) = lo;
-                } else {
-                    for (int jl = 0; jl < nj; ++jl) row[jl] = (uint8_t)(O[jl][m] >> (8 * k));
-                }
-            }
-    }
-    __syncthreads();
-    const size_t cwb = g0 * 32;
-    for (int r = threadIdx.x; r < kParCw; r += 256) {
-        // workspace column -> codeword (PERM: tile-lane order of the pair kernel, 4l + j <-> 64j + l)
-        const size_t x = cwb + r;
-        const size_t k = PERM ? ((x & ~(size_t)255) | ((x & 3) << 6) | ((x >> 2) & 63)) : x;
-        if (k >= ncw) continue;
-        uint8_t *dst = parity + k * pstride;
-        const uint8_t *s8 = stage + (r >> 5) * kRegion + (r & 31) * NR;
-        if constexpr (NR % 8 == 0) {
-#pragma unroll
-            for (int o = 0; o < NR; o += 8) {
-                uint2 v = *reinterpret_cast<const uint2 *>(s8 + o);
-                __builtin_memcpy(dst + o, &v, 8);
-            }
-        } else if constexpr (NR % 4 == 0) {
-#pragma unroll
-            for (int o = 0; o < NR; o += 4) {
-                uint32_t v = *reinterpret_cast<const uint32_t *>(s8 + o);
-                __builtin_memcpy(dst + o, &v, 4);
-            }
-        } else {
-            for (int o = 0; o < NR; ++o) dst[o] = s8[o];
-        }
-    }
-}
-
 
 // 8-wave form of k_ps_parity: wave P computes parity symbols 4P..4P+3 (q_pass4), halving each
 // wave's share of the map and doubling the waves that hide the phases' latencies.
@@ -1185,41 +1159,29 @@ template <class C> bool ps_matches(const DevCodec &d) {
            d.poly == C::POLY;
 }
 
-// Syndrome kernel: 0 = pair (default), 3 = 4-wave group, 2 = 8-wave slices; EZRS_PS_VARIANT =
-// pair | group4 | slices selects one for comparison runs.
+// Kernels: 0 = tile kernel k_pt (default); 1 = the round-2 pair syndrome kernel + k_ps_parity8
+// (EZRS_PS_VARIANT=pair, comparison runs only).
 int ps_variant() {
     static const int v = [] {
         const char *e = getenv("EZRS_PS_VARIANT");
-        if (e && std::string(e) == "slices") return 2;
-        if (e && std::string(e) == "group4") return 3;
-        return 0;
+        return (e && std::string(e) == "pair") ? 1 : 0;
     }();
     return v;
 }
 
-// Workgroups per launch (persistent over tiles): 2 per CU for the 8-wave slices and the 4-wave
-// group kernels (64 KiB LDS each), 4 per CU for the pair kernel (32 KiB each).
+// Workgroups per launch (persistent over tiles): tile kernel 2 per CU (80 KiB LDS each), pair
+// kernel 4 per CU (32 KiB each).
 unsigned syn_grid(const DevCodec &d, uint32_t ntiles, int var) {
-    const uint32_t per_cu = var == 0 ? 4u : 2u;
+    const uint32_t per_cu = var == 0 ? 2u : 4u;
     const uint32_t nwg = per_cu * (uint32_t)(d.ncu > 0 ? d.ncu : 256);
     return ntiles < nwg ? ntiles : nwg;
-}
-
-template <class C, bool ENC>
-void launch_syn(int var, unsigned grid, const ps::PsArgs &p, hipStream_t s) {
-    if (var == 0)
-        hipLaunchKernelGGL((ps::k_py_syndromes<typename C::PY, ENC>), dim3(grid), dim3(128), 0, s, p);
-    else if (var == 3)
-        hipLaunchKernelGGL((ps::k_pg_syndromes<typename C::PG4, ENC>), dim3(grid), dim3(256), 0, s, p);
-    else
-        hipLaunchKernelGGL((ps::k_ps_syndromes<typename C::PS, ENC>), dim3(grid), dim3(ps::kThreads), 0, s, p);
 }
 
 #define EZRS_PS_TRIPLE(C)                                                                         \
     struct T_##C {                                                                                \
         using PS = ps::PS_##C;                                                                    \
         using PY = ps::PY_##C;                                                                    \
-        using PG4 = ps::PG4_##C;                                                                  \
+        using PT = ps::PT_##C;                                                                    \
     };
 EZRS_PS_CODEC_LIST(EZRS_PS_TRIPLE)
 #undef EZRS_PS_TRIPLE
@@ -1236,13 +1198,30 @@ int planeslice_codec_id(const DevCodec &d) {
     return found;
 }
 
-// Encode workspace: [NR][ws_pitch] bytes, ws_pitch = ncw rounded up to 2048 (the parity kernel's
-// block); >= 32 bytes per codeword as decode needs.
+// Timing experiments only: EZRS_PT_ABLATE disables phases of the tile kernel (PsArgs::ablate).
+static int pt_ablate() {
+    const char *e = getenv("EZRS_PT_ABLATE");
+    return e ? atoi(e) : 0;
+}
+
+// The linear tile kernel needs an odd row pitch (conflict-free row reads); EZRS_PT_GATHER=1 keeps
+// the gather kernel for every pitch (comparison runs).
+static bool pt_linear(uint32_t stride) {
+    static const bool gather = [] {
+        const char *e = getenv("EZRS_PT_GATHER");
+        return e && *e == '1';
+    }();
+    return (stride & 1) && !gather;
+}
+
+// Workspace: decode [ncw][32] flagged syndromes; encode [NR][ws_pitch] syndromes, ws_pitch = ncw
+// rounded up to 2048 (the parity kernel's block).
 static size_t ps_pitch(size_t ncw) { return (ncw + 2047) / 2048 * 2048; }
 size_t ps_ws_bytes(size_t ncw) { return ps_pitch(ncw) * 32; }
 
-// Largest batch one launch takes: the tile span must stay below 4 GiB (32-bit buffer offsets).
-static size_t ps_max_rows(size_t stride) { return ((size_t)0xF0000000u / stride) / 2048 * 2048; }
+// Largest batch one launch takes: every buffer offset stays below 0xF0000000 (32-bit offsets;
+// the tile kernel's out-of-range marker kOob is above them).
+static size_t ps_max_rows(size_t stride) { return ((size_t)0xE0000000u / stride) / 2048 * 2048; }
 
 bool ps_can_encode(const DevCodec &, const EncodeArgs &a) {
     return a.data_stride >= 1 && a.data_stride <= 256;
@@ -1254,7 +1233,8 @@ bool ps_can_decode(const DevCodec &d, const DecodeArgs &a) {
 }
 
 hipError_t launch_ps_encode(int id, const DevCodec &d, const EncodeArgs &a, void *ws, hipStream_t s) {
-    const size_t maxr = ps_max_rows(a.data_stride);
+    const size_t pitch = a.data_stride > a.parity_stride ? a.data_stride : a.parity_stride;
+    const size_t maxr = ps_max_rows(pitch);
     const int var = ps_variant();
     for (size_t k0 = 0; k0 < a.ncw; k0 += maxr) {
         const size_t n = a.ncw - k0 < maxr ? a.ncw - k0 : maxr;
@@ -1266,18 +1246,28 @@ hipError_t launch_ps_encode(int id, const DevCodec &d, const EncodeArgs &a, void
         p.ntiles = (uint32_t)((n + ps::kTile - 1) / ps::kTile);
         p.lo = (int)(d.load - a.len);              // leading zero positions of a shortened code
         p.hi = (int)d.load;                        // data positions only
+        uint8_t *par = static_cast<uint8_t *>(a.parity) + k0 * a.parity_stride;
+        p.parity = par;
+        p.pstride = (uint32_t)a.parity_stride;
+        p.pspan = (uint32_t)((n - 1) * a.parity_stride + d.nroots);
         p.ws = static_cast<uint8_t *>(ws);
         p.ws_pitch = ps_pitch(n);
-        uint8_t *par = static_cast<uint8_t *>(a.parity) + k0 * a.parity_stride;
+        p.ablate = pt_ablate();
         const unsigned grid = syn_grid(d, p.ntiles, var);
-        const unsigned pgrid = (unsigned)((n + ps::kParCw - 1) / ps::kParCw);
+        const bool lin = pt_linear(p.stride);
         int k = 0;
-        // syndromes of the data positions, then parity = V^-1 S (the pair and group kernels leave
-        // the workspace in tile-lane column order: PERM)
 #define EZRS_PS_ENC(C)                                                                            \
         if (k++ == id) {                                                                          \
-            launch_syn<T_##C, true>(var, grid, p, s);                                             \
-            if (var == 2)                                                                         \
+            const unsigned pgrid = (unsigned)((n + ps::kParCw - 1) / ps::kParCw);                 \
+            if (var == 0 && lin)                                                                  \
+                hipLaunchKernelGGL((ps::pt::k_pt_lin<ps::PT_##C, true>), dim3(grid), dim3(ps::pt::kThreads), \
+                                   0, s, p);                                                      \
+            else if (var == 0)                                                                    \
+                hipLaunchKernelGGL((ps::pt::k_pt<ps::PT_##C, true>), dim3(grid), dim3(ps::pt::kThreads), \
+                                   0, s, p);                                                      \
+            else                                                                                  \
+                hipLaunchKernelGGL((ps::k_py_syndromes<ps::PY_##C, true>), dim3(grid), dim3(128), 0, s, p); \
+            if (var == 0 && lin)                                                                  \
                 hipLaunchKernelGGL((ps::k_ps_parity8<ps::PS_##C, false>), dim3(pgrid), dim3(512), 0, s, \
                                    static_cast<const uint8_t *>(ws), p.ws_pitch, par, a.parity_stride, n); \
             else                                                                                  \
@@ -1306,13 +1296,26 @@ hipError_t launch_ps_syndromes(int id, const DevCodec &d, const DecodeArgs &a, u
         p.ntiles = (uint32_t)((n + ps::kTile - 1) / ps::kTile);
         p.lo = (int)(d.load - a.len);
         p.hi = ps::kN;
-        p.neras = a.neras ? a.neras + k0 : nullptr;
+        // the tile kernel flags nonzero syndromes only; the error path adds the codewords with
+        // erasures (their syndromes are zero when the result slot holds 0)
+        p.neras = var == 0 ? nullptr : (a.neras ? a.neras + k0 : nullptr);
         p.result = a.result + k0;
         p.ws = syn_ws + k0 * 32;
+        p.ablate = pt_ablate();
         const unsigned grid = syn_grid(d, p.ntiles, var);
+        const bool lin = pt_linear(p.stride);
         int k = 0;
 #define EZRS_PS_SYN(C)                                                                            \
-        if (k++ == id) launch_syn<T_##C, false>(var, grid, p, s);
+        if (k++ == id) {                                                                          \
+            if (var == 0 && lin)                                                                  \
+                hipLaunchKernelGGL((ps::pt::k_pt_lin<ps::PT_##C, false>), dim3(grid), dim3(ps::pt::kThreads), \
+                                   0, s, p);                                                      \
+            else if (var == 0)                                                                    \
+                hipLaunchKernelGGL((ps::pt::k_pt<ps::PT_##C, false>), dim3(grid), dim3(ps::pt::kThreads), \
+                                   0, s, p);                                                      \
+            else                                                                                  \
+                hipLaunchKernelGGL((ps::k_py_syndromes<ps::PY_##C, false>), dim3(grid), dim3(128), 0, s, p); \
+        }
         EZRS_PS_CODEC_LIST(EZRS_PS_SYN)
 #undef EZRS_PS_SYN
         hipError_t e = hipGetLastError();

@@ -150,6 +150,8 @@ def _host_rows(a, what, itemsize, ndim=2):
         raise EzrsError(f"{what}: expected a {ndim}-D array with contiguous rows")
     if ndim == 1 and a.strides[0] != itemsize:
         raise EzrsError(f"{what}: expected a contiguous array")
+    if ndim == 2 and a.strides[0] < 0:
+        raise EzrsError(f"{what}: rows in reverse order (negative row stride) are not supported")
     return a.strides[0] // itemsize if ndim == 2 else 1
 
 
