@@ -991,7 +991,7 @@ def gen_pz(c: PsCodec):
 
 # ---- tile kernel (k_pt): 8 waves share one 256-codeword tile ------------------------------------
 PT_WAVES = 8
-PT_XCAP = 3               # items (8 words each) a wave sends per exchange sub-round (48 KiB area)
+PT_XCAP = 5               # items (8 words each) a wave sends per exchange sub-round (80 KiB area)
 
 
 def pt_exchange(groups_need, qn):

@@ -48,12 +48,21 @@ constexpr int kN = 255;
 
 typedef __attribute__((address_space(3))) void lds_void;
 
+#ifndef EZRS_PT_PRIO
+#define EZRS_PT_PRIO 0
+#endif
 #ifdef EZRS_PS_STAMPS
 __device__ unsigned long long g_py_stamps[16][2][8][8];  // [wg][wave][tile][phase]
 #define PY_STAMP(ph) do { __builtin_amdgcn_sched_barrier(0); if (blockIdx.x < 16 && it < 8 && lane == 0) \
     g_py_stamps[blockIdx.x][Q][it][ph] = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
+// tools/micro/pt_stamps.hip: phase stamps of the linear tile kernel, [wg][wave][tile][phase]
+__device__ unsigned long long g_pt_stamps[16][8][8][8];
+#define PT_STAMP(ph) do { __builtin_amdgcn_sched_barrier(0); if (blockIdx.x < 16 && pt_it < 8 && \
+    __lane_id() == 0) g_pt_stamps[blockIdx.x][pt_w][pt_it][ph] = __builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0); } while (0)
 #else
 #define PY_STAMP(ph) do { } while (0)
+#define PT_STAMP(ph) do { } while (0)
 #endif
 
 struct PsArgs {
@@ -427,14 +436,12 @@ __device__ __forceinline__ uint32_t gather4(uint32_t a0, uint32_t a1, uint32_t a
 namespace pt {
 
 constexpr int kThreads = 512;
-constexpr int kHalf = 32768;                  // one half image: 128 positions x 256 rows
-constexpr int kLds = 2 * kHalf + 16384;       // + exchange extension: 80 KiB, two workgroups per CU
-constexpr int kFlags = 2 * kHalf;             // decode flags [8][64] (extension, after the exchange)
+constexpr int kLds = 81920;                   // 80 KiB: two workgroups per CU
+constexpr int kGuard = 256;                   // bytes before the image: row 0's pad positions
+constexpr int kImage = 65536;                 // the tile image (256 rows x pitch <= 256 B)
+constexpr int kFlags = kGuard + kImage;       // decode flags [8][64] after the image
 constexpr uint32_t kOob = 0xF0000000u;        // a buffer offset past every span (ps_max_rows)
-#ifndef EZRS_PT_PREFETCH
-#define EZRS_PT_PREFETCH 0
-#endif
-constexpr bool kPrefetch = EZRS_PT_PREFETCH;   // next piece's reads during the current one's 2nd block
+static_assert(kFlags + 2048 <= kLds, "tile kernel LDS");
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
@@ -445,45 +452,7 @@ __device__ __forceinline__ uint32_t fresh(uint32_t = 0) {
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
     return l;
 }
-// This lane's byte of piece p (0..7) of a half image, row block 0.
-__device__ __forceinline__ uint32_t piece_addr(uint32_t lbuf, uint32_t lane, int p) {
-    const uint32_t l = fresh(lane);
-    return lbuf + 1024u * (l >> 3) + 128u * (l & 7) + ((16u * p) ^ (16u * ((l >> 1) & 7)));
-}
 
-// LDS image of half h: piece p (16 positions) of row 64k + l at
-//   h kHalf + 8 KiB k + 1 KiB (l >> 3) + 128 (l & 7) + 16 (p ^ ((l >> 1) & 7)),
-// written by DMA instruction i = 8k + m (rows 64k + 8m .. +7, 1 KiB at h kHalf + i KiB): lane j
-// loads row 64k + 8m + j/8, piece (j & 7) ^ f(8m + j/8).  Wave w issues i = 4w .. 4w + 3.
-__device__ __forceinline__ void issue_half(uint32_t lbuf, pw_rsrc_t rsrc, uint32_t toff, int h, int lo,
-                                           uint32_t stride, int w, int ablate = 0) {
-    if (ablate & 8) return;
-    const uint32_t base = toff + 128u * h - (uint32_t)lo;
-    const uint32_t l = fresh();
-    const uint32_t dslot = l >> 3;
-    const uint32_t k = (uint32_t)w >> 1;
-#pragma unroll
-    for (int ii = 0; ii < 4; ++ii) {
-        const uint32_t m = 4u * (w & 1) + ii;
-        const uint32_t p = (l & 7) ^ ((4u * (ii & 1) + (dslot >> 1)) & 7);
-        const uint32_t off = base + (64u * k + 8u * m + dslot) * stride + 16u * p;
-        asm volatile("s_mov_b32 m0, %0\n\t"
-                     "s_nop 0\n\t"
-                     "buffer_load_dwordx4 %1, %2, 0 offen lds"
-                     :: "s"(lbuf + h * kHalf + (8u * k + m) * 1024u), "v"(off), "s"(rsrc) : "memory", "m0");
-    }
-}
-
-__device__ __forceinline__ void read_piece(u32x4 (&R)[4], uint32_t addr) {
-    asm volatile("ds_read_b128 %0, %4\n\t"
-                 "ds_read_b128 %1, %4 offset:8192\n\t"
-                 "ds_read_b128 %2, %4 offset:16384\n\t"
-                 "ds_read_b128 %3, %4 offset:24576"
-                 : "=&v"(R[0]), "=&v"(R[1]), "=&v"(R[2]), "=&v"(R[3]) : "v"(addr) : "memory");
-}
-__device__ __forceinline__ void wait_piece(u32x4 (&R)[4]) {
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]) :: "memory");
-}
 template <int N> __device__ __forceinline__ void wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");
 }
@@ -497,131 +466,6 @@ __device__ __forceinline__ void store_byte(pw_rsrc_t r, uint32_t off, uint32_t v
     asm volatile("buffer_store_byte %0, %1, %2, 0 offen" :: "v"(v), "v"(off), "s"(r) : "memory");
 }
 
-// Block b of piece I of group G's quarter-0 waves, applied at this wave's piece (quarter q): the
-// network of block B0 on positions pa .. pa+7, pa = 16 (p0 + q) + 8 b; positions >= HI (beyond
-// the codeword, or the parity positions when encoding) contribute nothing.
-template <class C, int G, int HI, int P0, int B>
-__device__ __forceinline__ void block8(uint32_t (&V)[C::NI][8], uint32_t (&X)[8], int q) {
-    constexpr int lo_pa = 16 * P0 + 8 * B;                        // quarter 0
-    constexpr int hi_pa = 16 * (P0 + C::QN - 1) + 8 * B;          // last quarter
-    if constexpr (lo_pa < HI) {
-        if constexpr (hi_pa + 8 > HI) {                           // some quarter reaches HI
-            const int d = HI - (16 * (P0 + q) + 8 * B);            // wave-uniform
-            if (d <= 0) return;
-            if (d < 8) {
-#pragma unroll
-                for (int t = 0; t < 8; ++t)
-                    if (t >= d) X[t] = 0;
-            }
-        }
-        C::template block<G, 2 * P0 + B>(V, X);
-    }
-}
-
-// The pieces of half H of group G's waves at quarter q: quarter 0's pieces PIECE[G][I] + q.
-// Software-pipelined LDS reads when kPrefetch (the next piece's ds_reads in flight during the
-// current piece's second block).
-template <class C, int G, int H, int HI>
-__device__ __forceinline__ void half_pass(uint32_t (&V)[C::NI][8], uint32_t lbuf, int q) {
-    constexpr int I0 = H == 0 ? 0 : C::NP0[G];
-    constexpr int I1 = H == 0 ? C::NP0[G] : C::NP0[G] + C::NP1[G];
-    if constexpr (I1 > I0 && 16 * C::PIECE[G][I0] < HI) {
-        u32x4 R[4];
-        read_piece(R, piece_addr(lbuf + H * kHalf, 0, (C::PIECE[G][I0] + q) & 7));
-        static_for<I0, I1>([&](auto Ic) {
-            constexpr int I = decltype(Ic)::value;
-            constexpr int p0 = C::PIECE[G][I];
-            wait_piece(R);
-            uint32_t X[8];
-            {
-                const uint32_t c0[4] = {R[0].x, R[1].x, R[2].x, R[3].x};
-                const uint32_t c1[4] = {R[0].y, R[1].y, R[2].y, R[3].y};
-                transpose4x4(c0, X);
-                transpose4x4(c1, X + 4);
-            }
-            block8<C, G, HI, p0, 0>(V, X, q);
-            {
-                const uint32_t c2[4] = {R[0].z, R[1].z, R[2].z, R[3].z};
-                const uint32_t c3[4] = {R[0].w, R[1].w, R[2].w, R[3].w};
-                transpose4x4(c2, X);
-                transpose4x4(c3, X + 4);
-            }
-            if constexpr (I + 1 < I1 && kPrefetch) {
-                read_piece(R, piece_addr(lbuf + H * kHalf, 0, (C::PIECE[G][I + 1] + q) & 7));
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            block8<C, G, HI, p0, 1>(V, X, q);
-            if constexpr (I + 1 < I1 && !kPrefetch)
-                read_piece(R, piece_addr(lbuf + H * kHalf, 0, (C::PIECE[G][I + 1] + q) & 7));
-        });
-    }
-}
-
-// Positions before lo are the zero pad of a shortened code; the row windows fill them with the
-// previous row's bytes.  Each wave zeroes them in the pieces of half H it reads (every wave that
-// reads a piece writes the same bytes), after the half landed and before any read of it.
-template <class C, int G, int H>
-__device__ __forceinline__ void zero_pad(uint32_t lbuf, int q, int lo) {
-    constexpr int I0 = H == 0 ? 0 : C::NP0[G];
-    constexpr int I1 = H == 0 ? C::NP0[G] : C::NP0[G] + C::NP1[G];
-#pragma unroll 1
-    for (int i = I0; i < I1; ++i) {
-        const int pc = C::PIECE[G][i] + q;
-        const int n = lo - 16 * pc;                          // leading positions of the piece to clear
-        if (n <= 0) continue;                                // wave-uniform
-        const uint32_t at = piece_addr(lbuf + H * kHalf, 0, pc & 7);
-#pragma unroll 1
-        for (int k = 0; k < 4; ++k) {
-            u32x4 v = {0u, 0u, 0u, 0u};
-            if (n < 16) {
-                asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)"
-                             : "=&v"(v) : "v"(at + 8192u * k) : "memory");
-#pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    const int z = n - 4 * d;                 // bytes of dword d to clear
-                    const uint32_t m = z >= 4 ? 0u : z <= 0 ? ~0u : ~0u << (8 * z);
-                    v[d] &= m;
-                }
-            }
-            asm volatile("ds_write_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" :: "v"(at + 8192u * k), "v"(v) : "memory");
-        }
-    }
-}
-
-// Pieces of half H that straddle the span's ends come back all-zero from the buffer load: re-read
-// their bytes one by one (first / last tile of a launch only; out-of-range bytes read as zero).
-// Every wave that reads a piece patches it itself, with the same bytes.  Offsets are 32-bit: a
-// "negative" offset (row 0 of a shortened code) wraps above every span.
-template <class C, int G, int H>
-__device__ __forceinline__ void fix_half(const PsArgs &a, pw_rsrc_t rsrc, uint32_t toff, uint32_t lbuf, int q) {
-    constexpr int I0 = H == 0 ? 0 : C::NP0[G];
-    constexpr int I1 = H == 0 ? C::NP0[G] : C::NP0[G] + C::NP1[G];
-#pragma unroll 1
-    for (int i = I0 * 4; i < I1 * 4; ++i) {
-        const int k = i & 3, p = (C::PIECE[G][i >> 2] + q) & 7;
-        const uint32_t o = toff + (64u * k + fresh()) * a.stride + 128u * H + 16u * p - (uint32_t)a.lo;
-        const bool straddle = o >= 0xFFFFFFF1u || (o < a.span && o + 16u > a.span);
-        if (!straddle) continue;
-        const uint32_t dst = piece_addr(lbuf + H * kHalf, 0, p) + 8192u * k;
-#pragma unroll 1
-        for (int j = 0; j < 16; ++j) {
-            uint32_t v;
-            asm volatile("buffer_load_ubyte %0, %1, %2, 0 offen\n\ts_waitcnt vmcnt(0)"
-                         : "=&v"(v) : "v"(o + j), "s"(rsrc) : "memory");
-            asm volatile("ds_write_b8 %0, %1\n\ts_waitcnt lgkmcnt(0)" :: "v"(dst + j), "v"(v) : "memory");
-        }
-    }
-}
-
-// One half of the tile for group G: fix-ups, then the pieces.
-template <class C, int G, int H, int HI>
-__device__ __forceinline__ void do_half(uint32_t (&V)[C::NI][8], const PsArgs &a, pw_rsrc_t rsrc,
-                                        uint32_t toff, uint32_t lbuf, int q, bool edge) {
-    if (__builtin_expect(edge, 0)) fix_half<C, G, H>(a, rsrc, toff, lbuf, q);
-    if (a.lo > 128 * H) zero_pad<C, G, H>(lbuf, q, a.lo);
-    half_pass<C, G, H, HI>(V, lbuf, q);
-}
-
 // Recursive-halving exchange, sub-rounds S.. (see gen_ps.py PtRole): send the XS items to the
 // area, then add the partner's XV items.  lx = this lane's byte in wave 0's slot 0.
 template <class C, int W, int S, int J = 0>
@@ -633,8 +477,8 @@ __device__ __forceinline__ void xsend(uint32_t (&V)[C::NI][8], uint32_t lx) {
             const u32x4 w1 = {V[it][4], V[it][5], V[it][6], V[it][7]};
             asm volatile("ds_write_b128 %0, %1 offset:%3\n\t"
                          "ds_write_b128 %0, %2 offset:%4"
-                         :: "v"(lx), "v"(w0), "v"(w1), "n"((W * C::XCAP + J) * 2048),
-                            "n"((W * C::XCAP + J) * 2048 + 1024) : "memory");
+                         :: "v"(lx + W * C::XCAP * 2048u), "v"(w0), "v"(w1), "n"(J * 2048),
+                            "n"(J * 2048 + 1024) : "memory");
         }
         xsend<C, W, S, J + 1>(V, lx);
     }
@@ -649,8 +493,8 @@ __device__ __forceinline__ void xrecv(uint32_t (&V)[C::NI][8], uint32_t lx) {
             asm volatile("ds_read_b128 %0, %2 offset:%3\n\t"
                          "ds_read_b128 %1, %2 offset:%4\n\t"
                          "s_waitcnt lgkmcnt(0)"
-                         : "=&v"(w0), "=&v"(w1) : "v"(lx), "n"((PW * C::XCAP + J) * 2048),
-                           "n"((PW * C::XCAP + J) * 2048 + 1024) : "memory");
+                         : "=&v"(w0), "=&v"(w1) : "v"(lx + PW * C::XCAP * 2048u), "n"(J * 2048),
+                           "n"(J * 2048 + 1024) : "memory");
             V[it][0] ^= w0.x; V[it][1] ^= w0.y; V[it][2] ^= w0.z; V[it][3] ^= w0.w;
             V[it][4] ^= w1.x; V[it][5] ^= w1.y; V[it][6] ^= w1.z; V[it][7] ^= w1.w;
         }
@@ -669,151 +513,13 @@ __device__ __forceinline__ void exchange(uint32_t (&V)[C::NI][8], uint32_t lx) {
     }
 }
 
-// Stores of one tile's epilogue, the same count for every wave so that every vmcnt is a
-// compile-time constant: decode, 4 results + one byte store per syndrome slot (4 x 4) and codeword
-// of the lane (flagged codewords only; the others and the empty slots go out of range); encode,
-// one dword per syndrome slot (the lane's 4 codewords' bytes, tile-lane column order).
-template <bool ENC> constexpr int n_stores() { return ENC ? 4 : 4 + 16; }
-
-// Fix-up, exchange, fold and stores of wave W (its own tables and epilogue).
-template <class C, bool ENC, int W>
-__device__ __forceinline__ void wave_tail(uint32_t (&V)[C::NI][8], const PsArgs &a, uint32_t lbuf, uint32_t tile,
-                                          uint32_t noff, pw_rsrc_t rsrc, pw_rsrc_t rout, pw_rsrc_t rws) {
-    constexpr int G = W % C::GN, Q = W / C::GN;
-    if (!(a.ablate & 2)) {
-        if constexpr (Q > 0) C::template fix<G, Q>(V);      // quarter 0's weights -> this quarter's
-        // exchange through the half-1 image + extension: wave W's slot j at (W XCAP + j) 2 KiB
-        exchange<C, W, 0>(V, lbuf + kHalf + 16u * fresh());
-    }
-    issue_half(lbuf, rsrc, noff, 1, a.lo, a.stride, W, a.ablate);    // the next tile's half 1
-    uint32_t T[C::NOWN][8];
-#pragma unroll
-    for (int i = 0; i < C::NOWN; ++i)
-#pragma unroll
-        for (int t = 0; t < 8; ++t) T[i][t] = C::OWN[W][i] >= 0 ? V[C::OWN[W][i] < 0 ? 0 : C::OWN[W][i]][t] : 0u;
-    uint32_t Qs[8] = {0, 0, 0, 0, 0, 0, 0, 0}, nz = 0;
-    constexpr uint32_t vm = (C::SYN[W][0][0] >= 0 ? 0x01010101u : 0u) | (C::SYN[W][0][1] >= 0 ? 0x02020202u : 0u) |
-                            (C::SYN[W][0][2] >= 0 ? 0x04040404u : 0u) | (C::SYN[W][0][3] >= 0 ? 0x08080808u : 0u);
-    if (!(a.ablate & 4))
-        C::template epilogue<W>(T, [&](auto, uint32_t (&Qw)[8]) {
-#pragma unroll
-            for (int t = 0; t < 8; ++t) {
-                nz |= Qw[t] & vm;
-                Qs[t] = Qw[t];
-            }
-        });
-    if constexpr (ENC) {
-        transpose8(Qs);                                      // Qs[jj] byte k: syndrome jj, codeword k
-        // column tile 256 + 4 l + k <-> codeword tile 256 + 64 k + l (k_ps_parity8<PERM>)
-        const uint32_t col = tile * kTile + 4u * fresh();
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj)
-            store_dword(rws, C::SYN[W][0][jj] >= 0 ? (uint32_t)(C::SYN[W][0][jj] * a.ws_pitch) + col : kOob, Qs[jj]);
-    } else {
-        uint32_t fl = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (nz >> (8 * k) & 0xFF) fl |= 1u << k;
-        // OR over the 8 waves
-        const uint32_t fa = lbuf + kFlags + 256u * W + 4u * fresh();
-        asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" :: "v"(fa), "v"(fl) : "memory");
-        barrier();
-        {
-            uint32_t f[8];
-            const uint32_t fb = lbuf + kFlags + 4u * fresh();
-            asm volatile("ds_read_b32 %0, %8\n\t"
-                         "ds_read_b32 %1, %8 offset:256\n\t"
-                         "ds_read_b32 %2, %8 offset:512\n\t"
-                         "ds_read_b32 %3, %8 offset:768\n\t"
-                         "ds_read_b32 %4, %8 offset:1024\n\t"
-                         "ds_read_b32 %5, %8 offset:1280\n\t"
-                         "ds_read_b32 %6, %8 offset:1536\n\t"
-                         "ds_read_b32 %7, %8 offset:1792\n\t"
-                         "s_waitcnt lgkmcnt(0)"
-                         : "=&v"(f[0]), "=&v"(f[1]), "=&v"(f[2]), "=&v"(f[3]), "=&v"(f[4]),
-                           "=&v"(f[5]), "=&v"(f[6]), "=&v"(f[7]) : "v"(fb) : "memory");
-            fl = f[0] | f[1] | f[2] | f[3] | f[4] | f[5] | f[6] | f[7];
-            if (a.ablate & 32) fl = 0;                       // timing runs: keep the error path idle
-        }
-        const uint32_t cw0 = tile * kTile + fresh();         // byte k <-> codeword cw0 + 64k
-        // results: wave 0 writes them, every other wave issues the same stores out of range
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            store_dword(rout, W == 0 ? (cw0 + 64u * k) * 4u : kOob, (fl >> k & 1) ? (uint32_t)kSentinel : 0u);
-        if (__ballot(fl != 0) != 0) transpose8(Qs);          // Qs[jj] byte k: syndrome jj, codeword k
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t row = (fl >> k & 1) ? (cw0 + 64u * k) * 32u : kOob;
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj)
-                store_byte(rws, C::SYN[W][0][jj] >= 0 ? row + C::SYN[W][0][jj] : kOob, Qs[jj] >> (8 * k));
-        }
-    }
-}
-
-// The tile loop of the waves of leader group G (wave w = G + GN q): one copy of the main loop per
-// group; the per-wave tails differ.
-template <class C, bool ENC, int G>
-__device__ __forceinline__ void pt_run(const PsArgs &a, uint8_t *lds, int w) {
-    constexpr int HI = ENC ? kN - (int)C::NR : kN;            // positions evaluated
-    constexpr int NST = n_stores<ENC>();
-    const int q = w / C::GN;
-    const pw_rsrc_t rsrc = pw_rsrc(a.base, a.span);
-    const uint32_t lbuf = __builtin_amdgcn_readfirstlane(lds_addr(lds));
-    const uint32_t tile_bytes = a.stride * kTile;
-    const pw_rsrc_t rout = pw_rsrc(reinterpret_cast<const uint8_t *>(a.result), ENC ? 0u : a.ncw * 4u);
-    // decode: [ncw][32] flagged syndromes; encode: [NR][ws_pitch] syndrome-major, tile-lane order
-    const pw_rsrc_t rws = pw_rsrc(a.ws, ENC ? (uint32_t)(C::NR * a.ws_pitch) : a.ncw * 32u);
-
-    uint32_t tile = blockIdx.x;
-    issue_half(lbuf, rsrc, tile * tile_bytes, 0, a.lo, a.stride, w, a.ablate);
-    issue_half(lbuf, rsrc, tile * tile_bytes, 1, a.lo, a.stride, w, a.ablate);
-    for (int it = 0; tile < a.ntiles; tile += gridDim.x, ++it) {
-        const uint32_t toff = tile * tile_bytes;
-        const bool more = tile + gridDim.x < a.ntiles;
-        const uint32_t noff = more ? toff + gridDim.x * tile_bytes : kOob;
-        const bool edge = (tile == 0 && (a.lo & 15)) || toff + tile_bytes + 256u > a.span;
-        uint32_t V[C::NI][8];
-#pragma unroll
-        for (int s = 0; s < C::NI; ++s)
-#pragma unroll
-            for (int t = 0; t < 8; ++t) V[s][t] = 0;
-        // half 0 landed (younger: this tile's half 1, the previous tile's stores)
-        if (it) wait_vm<4 + NST>(); else wait_vm<4>();
-        barrier();
-        if (!(a.ablate & 1)) do_half<C, G, 0, HI>(V, a, rsrc, toff, lbuf, q, edge);
-        barrier();                                           // half 0 consumed
-        issue_half(lbuf, rsrc, noff, 0, a.lo, a.stride, w, a.ablate);  // the next tile's half 0
-        // half 1 landed (younger: the previous tile's stores, the next tile's half 0)
-        if (it) wait_vm<4 + NST>(); else wait_vm<4>();
-        barrier();
-        if (!(a.ablate & 1)) do_half<C, G, 1, HI>(V, a, rsrc, toff, lbuf, q, edge);
-        barrier();                                           // half 1 consumed
-        static_assert(C::QN <= 8, "");
-        switch (q) {
-        case 0: wave_tail<C, ENC, G>(V, a, lbuf, tile, noff, rsrc, rout, rws); break;
-        case 1: if constexpr (C::QN > 1) wave_tail<C, ENC, G + C::GN>(V, a, lbuf, tile, noff, rsrc, rout, rws); break;
-        case 2: if constexpr (C::QN > 2) wave_tail<C, ENC, G + 2 * C::GN>(V, a, lbuf, tile, noff, rsrc, rout, rws); break;
-        case 3: if constexpr (C::QN > 3) wave_tail<C, ENC, G + 3 * C::GN>(V, a, lbuf, tile, noff, rsrc, rout, rws); break;
-        case 4: if constexpr (C::QN > 4) wave_tail<C, ENC, G + 4 * C::GN>(V, a, lbuf, tile, noff, rsrc, rout, rws); break;
-        case 5: if constexpr (C::QN > 5) wave_tail<C, ENC, G + 5 * C::GN>(V, a, lbuf, tile, noff, rsrc, rout, rws); break;
-        case 6: if constexpr (C::QN > 6) wave_tail<C, ENC, G + 6 * C::GN>(V, a, lbuf, tile, noff, rsrc, rout, rws); break;
-        default: if constexpr (C::QN > 7) wave_tail<C, ENC, G + 7 * C::GN>(V, a, lbuf, tile, noff, rsrc, rout, rws); break;
-        }
-    }
-    wait_vm<0>();                                            // no DMA may land after the exit
-}
-
-// ---- linear variant (odd row pitch): the whole tile by linear 1 KiB LDS-DMA ----------------------
 // The tile's rows are one contiguous span; 64 line-aligned 1 KiB DMA instructions copy it to LDS as
 // it lies (fetch-efficient: every 128-byte line is read once, by one instruction).  Lane l owns rows
 // 4l .. 4l+3 (byte k of its words = row 4l + k): with an odd pitch P the rows' starts 4lP fall in
 // 32 distinct LDS banks, so the row reads (ds_read2_b32, 4-byte aligned, then v_alignbyte by the
-// row's byte phase (kP - lo) mod 4) are conflict-free.  One tile buffer per workgroup; the other
-// workgroup on the CU computes while this one's next tile lands.
-constexpr int kGuard = 256;                      // bytes before the image: row 0's pad positions
-constexpr int kLinFlags = kGuard + 65536 + 64;   // decode flags [8][64] after the image
-static_assert(kLinFlags + 2048 <= kLds, "linear variant LDS");
+// row's byte phase (kP - lo) mod 4) are conflict-free (an even pitch is correct, with conflicts).
+// One tile buffer per workgroup; the other workgroup on the CU computes while this one's next tile
+// lands.  The exchange uses the whole 80 KiB once the image is consumed.
 
 __device__ __forceinline__ void issue_tile_lin(uint32_t lbuf, pw_rsrc_t rsrc, uint32_t toff, uint32_t tile_bytes,
                                                int w, int ablate) {
@@ -904,12 +610,15 @@ __device__ __forceinline__ void lin_pass(uint32_t (&V)[C::NI][8], uint32_t lbuf,
 template <class C, bool ENC, int W>
 __device__ __forceinline__ void wave_tail_lin(uint32_t (&V)[C::NI][8], const PsArgs &a, uint32_t lbuf,
                                               uint32_t tile, uint32_t noff, uint32_t tile_bytes,
-                                              pw_rsrc_t rsrc, pw_rsrc_t rout, pw_rsrc_t rws) {
+                                              pw_rsrc_t rsrc, pw_rsrc_t rout, pw_rsrc_t rws, int pt_it = 0) {
+    const int pt_w = W;
+    (void)pt_it; (void)pt_w;
     constexpr int G = W % C::GN, Q = W / C::GN;
     if (!(a.ablate & 2)) {
         if constexpr (Q > 0) C::template fix<G, Q>(V);      // quarter 0's weights -> this quarter's
-        exchange<C, W, 0>(V, lbuf + kGuard + 16u * fresh());
+        exchange<C, W, 0>(V, lbuf + 16u * fresh());         // slot (W XCAP + j) at 2 KiB each
     }
+    PT_STAMP(4);
     if (noff != kOob) issue_tile_lin(lbuf, rsrc, noff, tile_bytes, W, a.ablate);
     uint32_t T[C::NOWN][8];
 #pragma unroll
@@ -927,6 +636,7 @@ __device__ __forceinline__ void wave_tail_lin(uint32_t (&V)[C::NI][8], const PsA
                 Qs[t] = Qw[t];
             }
         });
+    PT_STAMP(5);
     const uint32_t cw0 = tile * kTile + 4u * fresh();        // byte k <-> codeword cw0 + k
     if constexpr (ENC) {
         transpose8(Qs);                                      // Qs[jj] byte k: syndrome jj, codeword k
@@ -939,12 +649,12 @@ __device__ __forceinline__ void wave_tail_lin(uint32_t (&V)[C::NI][8], const PsA
 #pragma unroll
         for (int k = 0; k < 4; ++k)
             if (nz >> (8 * k) & 0xFF) fl |= 1u << k;
-        const uint32_t fa = lbuf + kLinFlags + 256u * W + 4u * fresh();
+        const uint32_t fa = lbuf + kFlags + 256u * W + 4u * fresh();
         asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" :: "v"(fa), "v"(fl) : "memory");
         barrier();
         {
             uint32_t f[8];
-            const uint32_t fb = lbuf + kLinFlags + 4u * fresh();
+            const uint32_t fb = lbuf + kFlags + 4u * fresh();
             asm volatile("ds_read_b32 %0, %8\n\t"
                          "ds_read_b32 %1, %8 offset:256\n\t"
                          "ds_read_b32 %2, %8 offset:512\n\t"
@@ -975,6 +685,7 @@ __device__ __forceinline__ void wave_tail_lin(uint32_t (&V)[C::NI][8], const PsA
             }
         }
     }
+    PT_STAMP(6);
 }
 
 template <class C, bool ENC, int G>
@@ -987,7 +698,9 @@ __device__ __forceinline__ void pt_run_lin(const PsArgs &a, uint8_t *lds, int w)
     const pw_rsrc_t rws = pw_rsrc(a.ws, ENC ? (uint32_t)(C::NR * a.ws_pitch) : a.ncw * 32u);
     uint32_t tile = blockIdx.x;
     issue_tile_lin(lbuf, rsrc, tile * tile_bytes, tile_bytes, w, a.ablate);
-    for (; tile < a.ntiles; tile += gridDim.x) {
+    int pt_it = 0, pt_w = w;
+    (void)pt_it; (void)pt_w;
+    for (; tile < a.ntiles; tile += gridDim.x, ++pt_it) {
         // run-time values re-read each tile: nothing derived from them is hoisted out of the loop
         int q = w / C::GN, lo = a.lo;
         asm volatile("" : "+s"(q), "+s"(lo));
@@ -1001,8 +714,10 @@ __device__ __forceinline__ void pt_run_lin(const PsArgs &a, uint8_t *lds, int w)
         for (int s = 0; s < C::NI; ++s)
 #pragma unroll
             for (int t = 0; t < 8; ++t) V[s][t] = 0;
+        PT_STAMP(0);
         wait_vm<0>();                                        // the tile landed (and the stores went)
         barrier();
+        PT_STAMP(1);
         if (toff + tile_bytes > a.span) {                    // last tile: the span's final bytes
             // a 16-byte DMA piece that crosses the span's end comes back all-zero: re-read the last
             // 64 bytes one by one (out-of-range bytes read as zero)
@@ -1017,17 +732,27 @@ __device__ __forceinline__ void pt_run_lin(const PsArgs &a, uint8_t *lds, int w)
             }
             barrier();
         }
+#if EZRS_PT_PRIO
+        // main loop priority experiments (timing builds only): 1 = waves 4..7 first, 2 = by quarter
+        if (EZRS_PT_PRIO == 1 && w >= 4) asm volatile("s_setprio 1");
+        if (EZRS_PT_PRIO == 2) { if (w >= 6) asm volatile("s_setprio 3"); else if (w >= 4) asm volatile("s_setprio 2"); else if (w >= 2) asm volatile("s_setprio 1"); }
+#endif
         if (!(a.ablate & 1)) lin_pass<C, G, HI>(V, lbuf, a.stride, q, lo, ph);
+#if EZRS_PT_PRIO
+        asm volatile("s_setprio 0");
+#endif
+        PT_STAMP(2);
         barrier();                                           // the image is consumed
+        PT_STAMP(3);
         switch (w / C::GN) {
-        case 0: wave_tail_lin<C, ENC, G>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws); break;
-        case 1: if constexpr (C::QN > 1) wave_tail_lin<C, ENC, G + C::GN>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws); break;
-        case 2: if constexpr (C::QN > 2) wave_tail_lin<C, ENC, G + 2 * C::GN>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws); break;
-        case 3: if constexpr (C::QN > 3) wave_tail_lin<C, ENC, G + 3 * C::GN>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws); break;
-        case 4: if constexpr (C::QN > 4) wave_tail_lin<C, ENC, G + 4 * C::GN>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws); break;
-        case 5: if constexpr (C::QN > 5) wave_tail_lin<C, ENC, G + 5 * C::GN>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws); break;
-        case 6: if constexpr (C::QN > 6) wave_tail_lin<C, ENC, G + 6 * C::GN>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws); break;
-        default: if constexpr (C::QN > 7) wave_tail_lin<C, ENC, G + 7 * C::GN>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws); break;
+        case 0: wave_tail_lin<C, ENC, G>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws, pt_it); break;
+        case 1: if constexpr (C::QN > 1) wave_tail_lin<C, ENC, G + C::GN>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws, pt_it); break;
+        case 2: if constexpr (C::QN > 2) wave_tail_lin<C, ENC, G + 2 * C::GN>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws, pt_it); break;
+        case 3: if constexpr (C::QN > 3) wave_tail_lin<C, ENC, G + 3 * C::GN>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws, pt_it); break;
+        case 4: if constexpr (C::QN > 4) wave_tail_lin<C, ENC, G + 4 * C::GN>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws, pt_it); break;
+        case 5: if constexpr (C::QN > 5) wave_tail_lin<C, ENC, G + 5 * C::GN>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws, pt_it); break;
+        case 6: if constexpr (C::QN > 6) wave_tail_lin<C, ENC, G + 6 * C::GN>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws, pt_it); break;
+        default: if constexpr (C::QN > 7) wave_tail_lin<C, ENC, G + 7 * C::GN>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws, pt_it); break;
         }
     }
     wait_vm<0>();                                            // no DMA may land after the exit
@@ -1038,21 +763,11 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(kThreads, kThreads), 
 k_pt_lin(PsArgs a) {
     static_assert(C::NQ == 1, "one quad (4 syndromes) per wave");
     static_assert(C::GN <= 2 && C::GN * C::QN == 8, "8 waves: at most two leader groups");
+    static_assert(8 * C::XCAP * 2048 <= kLds, "exchange area");
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLds];
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (C::GN == 1 || w % C::GN == 0) pt_run_lin<C, ENC, 0>(a, lds, w);
     else pt_run_lin<C, ENC, C::GN - 1>(a, lds, w);
-}
-
-template <class C, bool ENC>
-__global__ void __attribute__((amdgpu_flat_work_group_size(kThreads, kThreads), amdgpu_waves_per_eu(4)))
-k_pt(PsArgs a) {
-    static_assert(C::NQ == 1, "one quad (4 syndromes) per wave");
-    static_assert(C::GN <= 2 && C::GN * C::QN == 8, "8 waves: at most two leader groups");
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kLds];
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (C::GN == 1 || w % C::GN == 0) pt_run<C, ENC, 0>(a, lds, w);
-    else pt_run<C, ENC, C::GN - 1>(a, lds, w);
 }
 
 } // namespace pt
@@ -1204,16 +919,6 @@ static int pt_ablate() {
     return e ? atoi(e) : 0;
 }
 
-// The linear tile kernel needs an odd row pitch (conflict-free row reads); EZRS_PT_GATHER=1 keeps
-// the gather kernel for every pitch (comparison runs).
-static bool pt_linear(uint32_t stride) {
-    static const bool gather = [] {
-        const char *e = getenv("EZRS_PT_GATHER");
-        return e && *e == '1';
-    }();
-    return (stride & 1) && !gather;
-}
-
 // Workspace: decode [ncw][32] flagged syndromes; encode [NR][ws_pitch] syndromes, ws_pitch = ncw
 // rounded up to 2048 (the parity kernel's block).
 static size_t ps_pitch(size_t ncw) { return (ncw + 2047) / 2048 * 2048; }
@@ -1254,25 +959,20 @@ hipError_t launch_ps_encode(int id, const DevCodec &d, const EncodeArgs &a, void
         p.ws_pitch = ps_pitch(n);
         p.ablate = pt_ablate();
         const unsigned grid = syn_grid(d, p.ntiles, var);
-        const bool lin = pt_linear(p.stride);
         int k = 0;
 #define EZRS_PS_ENC(C)                                                                            \
         if (k++ == id) {                                                                          \
             const unsigned pgrid = (unsigned)((n + ps::kParCw - 1) / ps::kParCw);                 \
-            if (var == 0 && lin)                                                                  \
+            if (var == 0) {                                                                       \
                 hipLaunchKernelGGL((ps::pt::k_pt_lin<ps::PT_##C, true>), dim3(grid), dim3(ps::pt::kThreads), \
                                    0, s, p);                                                      \
-            else if (var == 0)                                                                    \
-                hipLaunchKernelGGL((ps::pt::k_pt<ps::PT_##C, true>), dim3(grid), dim3(ps::pt::kThreads), \
-                                   0, s, p);                                                      \
-            else                                                                                  \
-                hipLaunchKernelGGL((ps::k_py_syndromes<ps::PY_##C, true>), dim3(grid), dim3(128), 0, s, p); \
-            if (var == 0 && lin)                                                                  \
                 hipLaunchKernelGGL((ps::k_ps_parity8<ps::PS_##C, false>), dim3(pgrid), dim3(512), 0, s, \
                                    static_cast<const uint8_t *>(ws), p.ws_pitch, par, a.parity_stride, n); \
-            else                                                                                  \
+            } else {                                                                              \
+                hipLaunchKernelGGL((ps::k_py_syndromes<ps::PY_##C, true>), dim3(grid), dim3(128), 0, s, p); \
                 hipLaunchKernelGGL((ps::k_ps_parity8<ps::PS_##C, true>), dim3(pgrid), dim3(512), 0, s, \
                                    static_cast<const uint8_t *>(ws), p.ws_pitch, par, a.parity_stride, n); \
+            }                                                                                     \
         }
         EZRS_PS_CODEC_LIST(EZRS_PS_ENC)
 #undef EZRS_PS_ENC
@@ -1303,15 +1003,11 @@ hipError_t launch_ps_syndromes(int id, const DevCodec &d, const DecodeArgs &a, u
         p.ws = syn_ws + k0 * 32;
         p.ablate = pt_ablate();
         const unsigned grid = syn_grid(d, p.ntiles, var);
-        const bool lin = pt_linear(p.stride);
         int k = 0;
 #define EZRS_PS_SYN(C)                                                                            \
         if (k++ == id) {                                                                          \
-            if (var == 0 && lin)                                                                  \
+            if (var == 0)                                                                         \
                 hipLaunchKernelGGL((ps::pt::k_pt_lin<ps::PT_##C, false>), dim3(grid), dim3(ps::pt::kThreads), \
-                                   0, s, p);                                                      \
-            else if (var == 0)                                                                    \
-                hipLaunchKernelGGL((ps::pt::k_pt<ps::PT_##C, false>), dim3(grid), dim3(ps::pt::kThreads), \
                                    0, s, p);                                                      \
             else                                                                                  \
                 hipLaunchKernelGGL((ps::k_py_syndromes<ps::PY_##C, false>), dim3(grid), dim3(128), 0, s, p); \
