@@ -471,49 +471,44 @@ def harness_check(args):
 
 
 def bench_shards(args):
-    """SURVEY.md 8d C2 shard batches: S-byte shards (S = 1 KiB .. 1 MiB) split into 223-byte data
-    chunks, each chunk + 32 parity bytes one RS(255,223) row, the last chunk of a shard shortened.
-    The full rows of every shard in the batch go in one call, the shortened tails in a second one
-    (the documented tail call; a shortened RS(255,223) row is a valid codeword of the same codec,
-    rs_base:1170-1242).  Batches are sized to ~256 MB of shard data per GPU (device-resident);
-    per S the line reports the encode+decode rate of shard bytes and each call's HBM fraction."""
+    """SURVEY.md 8d C2 shard batches: S-byte shards (S = 1 KiB .. 1 MiB) in the rsencode layout
+    (rsencode.C:93-163: 223-byte chunks, each followed by its 32 parity bytes, the last chunk
+    shortened), ~256 MB of shard data per GPU (device-resident).  The whole batch is one
+    ezrs_encode_shards and one ezrs_decode_shards call (one launch of the tile kernels each; the
+    shortened rows are handled inside them).  Per S the line reports the encode+decode rate of
+    shard bytes and each call's HBM fraction."""
     import torch
     import ezrs
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
     torch.cuda.set_device(local)
     codec = ezrs.Codec.rs(N, K, device=local)
     gen = torch.Generator(device="cuda").manual_seed(0x5EED0003)
     sweep = []
     for S in (1 << 10, 1 << 14, 1 << 18, 1 << 20):
         shards = max(1, (256 << 20) // S)
-        full, tail = S // K, S % K
-        rows = torch.randint(0, 256, (shards * full, N), generator=gen, device="cuda",
-                             dtype=torch.int32).to(torch.uint8)
-        trows = (torch.randint(0, 256, (shards, tail + NR), generator=gen, device="cuda",
-                               dtype=torch.int32).to(torch.uint8) if tail else None)
-        codec.reserve(max(rows.shape[0], shards))
-        r1 = torch.empty(rows.shape[0], dtype=torch.int32, device="cuda")
-        r2 = torch.empty(shards, dtype=torch.int32, device="cuda")
+        R = codec.shard_codewords(S)
+        enc = codec.shard_encoded_len(S)
+        buf = torch.randint(0, 256, (shards, enc), generator=gen, device="cuda",
+                            dtype=torch.int32).to(torch.uint8)
+        codec.reserve(shards * R)
+        res = torch.empty(shards * R, dtype=torch.int32, device="cuda")
         stream = torch.cuda.current_stream()
 
         def step(ev=None):
             if ev:
                 ev[0].record(stream)
-            codec.encode(rows, K, stream=stream)
-            if trows is not None:
-                codec.encode(trows, tail, stream=stream)
+            codec.encode_shards(buf, S, stream=stream)
             if ev:
                 ev[1].record(stream)
-            codec.decode(rows, K, result=r1, stream=stream)
-            if trows is not None:
-                codec.decode(trows, tail, result=r2, stream=stream)
+            codec.decode_shards(buf, S, result=res, stream=stream)
             if ev:
                 ev[2].record(stream)
         for _ in range(max(1, args.warmup)):
             step()
         torch.cuda.synchronize()
-        if int((r1 != 0).sum()) or (trows is not None and int((r2 != 0).sum())):
-            raise SystemExit(f"shards S={S}: encoded rows did not decode clean")
+        if int((res != 0).sum()):
+            raise SystemExit(f"shards S={S}: encoded shards did not decode clean")
         steps = max(1, args.steps)
         evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
         t0 = time.perf_counter()
@@ -523,22 +518,22 @@ def bench_shards(args):
         dt = (time.perf_counter() - t0) / steps
         enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / steps
         dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / steps
-        ncw_total = rows.shape[0] + (shards if tail else 0)
-        enc_alg = shards * (S + NR * (full + (1 if tail else 0)))    # data read + parity written
-        dec_alg = enc_alg + 4 * ncw_total                              # all read + result written
-        sweep.append({"shard_bytes": S, "shards": shards, "codewords": ncw_total,
-                      "tail_len": tail, "gbs_shard_data": round(shards * S / dt / 1e9, 3),
+        enc_alg = shards * enc                         # data read + parity written
+        dec_alg = enc_alg + 4 * shards * R             # all read + result written
+        sweep.append({"shard_bytes": S, "shards": shards, "codewords": shards * R,
+                      "tail_len": S - (R - 1) * K, "gbs_shard_data": round(shards * S / dt / 1e9, 3),
                       "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4),
                       "frac_encode": round(enc_alg / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                       "frac_decode": round(dec_alg / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
         log(f"shards S={S}: {sweep[-1]}")
-        del rows, trows
+        del buf
     best = max(sweep, key=lambda r: r["gbs_shard_data"])
     print(json.dumps({"metric": "RS(255,223) shard-batch encode+decode GB/s device-resident (sweep)",
-                      "value": best["gbs_shard_data"], "unit": "GB/s", "n_gpus": 1,
+                      "value": best["gbs_shard_data"], "unit": "GB/s", "n_gpus": world,
                       "steps": args.steps, "warmup": args.warmup, "higher_is_better": True,
                       "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-                      "config": {"workload": "C2 shard batches: S-byte shards, ~256 MB per step",
+                      "config": {"workload": "C2 shard batches: S-byte shards (rsencode layout), "
+                                             "~256 MB per step, one call per direction",
                                  "codec": "RS(255,223) poly 0x11d fcr 1 prim 1"},
                       "sweep": sweep}), flush=True)
 
@@ -557,7 +552,7 @@ def main():
                     help="c2: the headline RS(255,223) line; c1: the same for RS(255,251); c3: "
                          "RS(255,223) 8 errors + 4 erasures decode; c4: RS(65535,65503); c5: "
                          "BCH(1023,983,4) (SURVEY.md 8d); shards: RS(255,223) over S-byte shards, "
-                         "S = 1 KiB .. 1 MiB (full codewords + one shortened tail call per shard)")
+                         "S = 1 KiB .. 1 MiB (rsencode layout, one call per direction)")
     ap.add_argument("--harness-check", action="store_true",
                     help="CPU/gloo check of the multi-rank harness (placeholder step, no GPU)")
     args = ap.parse_args()

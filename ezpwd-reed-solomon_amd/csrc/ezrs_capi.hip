@@ -272,6 +272,7 @@ namespace {
 // ws: bs_encode_ws_bytes(ncw) bytes (bit-sliced path only).
 hipError_t dispatch_encode(const ezrs_codec *c, const EncodeArgs &a, void *ws, hipStream_t st) {
     if (c->ps_id >= 0 && ps_can_encode(c->dev, a)) return launch_ps_encode(c->ps_id, c->dev, a, ws, st);
+    if (a.sh.rows) return launch_encode_generic(c->dev, a, st);     // shard rows: per-codeword kernels
     if (c->wide_id >= 0 && wide_can_encode(c->dev, a))
         return launch_wide_encode(c->wide_id, c->dev, a, c->wide_blob.data(), c->d_wcols, ws, st);
     return c->bs_id >= 0 ? launch_bs_encode(c->bs_id, c->dev, a, ws, st) : launch_encode_generic(c->dev, a, st);
@@ -288,6 +289,7 @@ hipError_t dispatch_decode(const ezrs_codec *c, const DecodeArgs &a, uint8_t *sy
         if (e == hipSuccess) e = launch_decode_flagged(c->dev, a, syn_ws, st);
         return e;
     }
+    if (a.sh.rows) return launch_decode_generic(c->dev, a, st);     // shard rows: per-codeword kernels
     if (c->wide_id >= 0 && wide_can_decode(c->dev, a))
         return launch_wide_decode(c->wide_id, c->dev, a, c->wide_blob.data(), c->d_wcols, syn_ws, st);
     if (c->bs_id >= 0 && contiguous) {
@@ -446,6 +448,77 @@ int ezrs_decode(const ezrs_codec *c, void *data, size_t data_stride, unsigned le
     return ezrs_decode_ws(c, data, data_stride, len, parity, parity_stride, eras, eras_stride,
                           neras, result, positions, pos_stride, corr, corr_stride, ncw, ws, need,
                           stream);
+}
+
+// ---- shard batches -----------------------------------------------------------------------------
+namespace {
+
+// Rows per shard and the geometry of a shard batch (rsencode layout); false on bad arguments.
+bool shard_geom(const ezrs_codec *c, size_t shard_len, unsigned chunk, size_t shard_pitch, Shards &g) {
+    if (!c || shard_len == 0 || chunk == 0 || chunk > c->dev.load) return false;
+    const size_t R = (shard_len + chunk - 1) / chunk;
+    if (R > 0xFFFFFFFFu) return false;
+    const size_t enc = shard_len + R * c->dev.nroots;
+    if (shard_pitch < enc) return false;
+    g.rows = (uint32_t)R;
+    g.tail = (uint32_t)(shard_len - (R - 1) * chunk);
+    g.pitch = shard_pitch;
+    return true;
+}
+
+} // namespace
+
+size_t ezrs_shard_codewords(const ezrs_codec *c, size_t shard_len, unsigned chunk) {
+    if (!c || shard_len == 0 || chunk == 0 || chunk > c->dev.load) return 0;
+    return (shard_len + chunk - 1) / chunk;
+}
+
+size_t ezrs_shard_encoded_len(const ezrs_codec *c, size_t shard_len, unsigned chunk) {
+    const size_t R = ezrs_shard_codewords(c, shard_len, chunk);
+    return R ? shard_len + R * c->dev.nroots : 0;
+}
+
+int ezrs_encode_shards(const ezrs_codec *c, void *shards, size_t shard_pitch, size_t shard_len,
+                       unsigned chunk, size_t nshards, void *stream) {
+    Shards g;
+    if (!c || !shards || !shard_geom(c, shard_len, chunk, shard_pitch, g)) return -EINVAL;
+    if (nshards == 0) return 0;
+    const size_t w = c->dev.mm <= 8 ? 1 : 2, ncw = nshards * g.rows;
+    DeviceGuard dg(c->device);
+    const size_t need = ws_bytes_for(c, ncw);
+    void *ws = nullptr;
+    if (int r = stream_ws(c, stream, need, &ws)) return r;
+    char *r0 = static_cast<char *>(shards);
+    EncodeArgs a{r0, (size_t)chunk + c->dev.nroots, chunk, r0 + (size_t)chunk * w,
+                 (size_t)chunk + c->dev.nroots, ncw, g};
+    hipError_t e = dispatch_encode(c, a, ws, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return hip_fail(e, "encode launch");
+    return 0;
+}
+
+int ezrs_decode_shards(const ezrs_codec *c, void *shards, size_t shard_pitch, size_t shard_len,
+                       unsigned chunk, size_t nshards, const uint32_t *eras, size_t eras_stride,
+                       const uint32_t *neras, int32_t *result, uint32_t *positions,
+                       size_t pos_stride, void *corr, size_t corr_stride, void *stream) {
+    Shards g;
+    if (!c || !shards || !result || !shard_geom(c, shard_len, chunk, shard_pitch, g)) return -EINVAL;
+    if (nshards == 0) return 0;
+    const unsigned NR = c->dev.nroots;
+    const size_t w = c->dev.mm <= 8 ? 1 : 2, ncw = nshards * g.rows;
+    if (neras && !eras) return -EINVAL;
+    if (eras && ncw > 1 && eras_stride == 0) return -EINVAL;
+    if (positions && ncw > 1 && pos_stride < NR) return -EINVAL;
+    if (corr && ncw > 1 && corr_stride < NR) return -EINVAL;
+    DeviceGuard dg(c->device);
+    const size_t need = ws_bytes_for(c, ncw);
+    void *ws = nullptr;
+    if (int r = stream_ws(c, stream, need, &ws)) return r;
+    char *r0 = static_cast<char *>(shards);
+    DecodeArgs a{r0, (size_t)chunk + NR, chunk, r0 + (size_t)chunk * w, (size_t)chunk + NR, eras,
+                 eras_stride, neras, result, positions, pos_stride, corr, corr_stride, ncw, g};
+    hipError_t e = dispatch_decode(c, a, static_cast<uint8_t *>(ws), static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return hip_fail(e, "decode launch");
+    return 0;
 }
 
 // ---- host-memory pipeline ---------------------------------------------------------------------

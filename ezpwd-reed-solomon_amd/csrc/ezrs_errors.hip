@@ -332,8 +332,9 @@ __global__ void __launch_bounds__(64 * kWaves) k_decode_errors(DevCodec c, Decod
         for (unsigned c0 = 0; c0 < n; c0 += 64) {
             if (c0 + lane < n) {
                 const size_t k = sp * kSpan + W.list[c0 + lane];
-                uint8_t *data = static_cast<uint8_t *>(a.data) + k * a.data_stride;
-                uint8_t *parity = static_cast<uint8_t *>(a.parity) + k * a.parity_stride;
+                uint8_t *data, *parity;
+                unsigned len;
+                row_ptrs<uint8_t>(a, k, data, parity, len);
                 const uint32_t *eras = a.eras ? a.eras + k * a.eras_stride : nullptr;
                 const unsigned ne = a.neras ? a.neras[k] : 0;
                 uint32_t *pos = a.positions ? a.positions + k * a.pos_stride : nullptr;
@@ -341,7 +342,7 @@ __global__ void __launch_bounds__(64 * kWaves) k_decode_errors(DevCodec c, Decod
                 // a slot that does not hold the sentinel was flagged for its erasures only: its
                 // syndromes are zero and were not written
                 const bool synz = a.result[k] != kSentinel;
-                a.result[k] = decode_lane(c, L, W, lane, data, a.len, parity, eras, ne, pos, corr,
+                a.result[k] = decode_lane(c, L, W, lane, data, len, parity, eras, ne, pos, corr,
                                           synz ? nullptr : syn_ws + k * 32);
             }
         }

@@ -64,8 +64,10 @@ __global__ void __launch_bounds__(kBlock) k_encode_generic(DevCodec c, EncodeArg
     stage_tables<LDS>(c, smem, A, I, ID, FD);
     const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= a.ncw) return;
-    const T *data = static_cast<const T *>(a.data) + k * a.data_stride;
-    T *parity = static_cast<T *>(a.parity) + k * a.parity_stride;
+    const T *data;
+    T *parity;
+    unsigned len;
+    row_ptrs<T>(a, k, data, parity, len);
     const unsigned NR = c.nroots, nn = c.nn, mm = c.mm;
 
     // Circular parity register: logical parity[j] lives at par[(head + j) % NR], so the
@@ -77,7 +79,7 @@ __global__ void __launch_bounds__(kBlock) k_encode_generic(DevCodec c, EncodeArg
     uint16_t *const par = MAXR <= 32 ? pbuf + threadIdx.x : priv;
     for (unsigned j = 0; j < NR; ++j) par[(j) * PS] = 0;
     unsigned head = 0;
-    for (unsigned i = 0; i < a.len; ++i) {
+    for (unsigned i = 0; i < len; ++i) {
         unsigned sym = static_cast<unsigned>(data[i]) & nn;        // masked copy (rs_base:893)
         if (c.dual) sym = FD[sym];
         const unsigned fb = I[sym ^ par[(head) * PS]];
@@ -116,18 +118,20 @@ __global__ void __launch_bounds__(kBlock) k_encode_lanes(DevCodec c, EncodeArgs 
     const unsigned j = threadIdx.x & (kLaneGroup - 1);
     const size_t k = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / kLaneGroup;
     if (k >= a.ncw) return;                 // uniform over the group
-    const T *data = static_cast<const T *>(a.data) + k * a.data_stride;
-    T *parity = static_cast<T *>(a.parity) + k * a.parity_stride;
+    const T *data;
+    T *parity;
+    unsigned len;
+    row_ptrs<T>(a, k, data, parity, len);
     const unsigned NR = c.nroots, nn = c.nn;
     const unsigned g = j < NR ? c.genpoly[NR - 1 - j] : 0;
     unsigned par = 0;
-    for (unsigned i0 = 0; i0 < a.len; i0 += kLaneGroup) {
+    for (unsigned i0 = 0; i0 < len; i0 += kLaneGroup) {
         unsigned dv = 0;
-        if (i0 + j < a.len) {
+        if (i0 + j < len) {
             dv = static_cast<unsigned>(data[i0 + j]) & nn;            // masked copy (rs_base:893)
             if (c.dual) dv = FD[dv];
         }
-        const unsigned cnt = a.len - i0 < (unsigned)kLaneGroup ? a.len - i0 : kLaneGroup;
+        const unsigned cnt = len - i0 < (unsigned)kLaneGroup ? len - i0 : kLaneGroup;
         for (unsigned s = 0; s < cnt; ++s) {
             const unsigned sym = __shfl(dv, (int)s, kLaneGroup);
             const unsigned p0 = __shfl(par, 0, kLaneGroup);
@@ -411,11 +415,11 @@ __global__ void __launch_bounds__(kBlock) k_decode_lanes(DevCodec c, DecodeArgs 
     const unsigned j = threadIdx.x & (kLaneGroup - 1), grp = threadIdx.x / kLaneGroup;
     const size_t k = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / kLaneGroup;
     const bool valid = k < a.ncw;                       // uniform over the group
-    const unsigned NR = c.nroots, NN = c.nn, len = a.len;
+    const unsigned NR = c.nroots, NN = c.nn;
+    unsigned len = a.len;
     T *data = nullptr, *parity = nullptr;
     if (valid) {
-        data = static_cast<T *>(a.data) + k * a.data_stride;
-        parity = static_cast<T *>(a.parity) + k * a.parity_stride;
+        row_ptrs<T>(a, k, data, parity, len);
         const unsigned root = (unsigned)(((uint64_t)(c.fcr + j) * c.prim) % NN);
         const unsigned tot = len + NR;
         unsigned sv = 0;
@@ -467,18 +471,19 @@ __global__ void __launch_bounds__(kBlock) k_decode_generic(DevCodec c, DecodeArg
     stage_tables<LDS>(c, smem, A, I, ID, FD);
     const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= a.ncw) return;
-    T *data = static_cast<T *>(a.data) + k * a.data_stride;
-    T *parity = static_cast<T *>(a.parity) + k * a.parity_stride;
+    T *data, *parity;
+    unsigned len;
+    row_ptrs<T>(a, k, data, parity, len);
     const uint32_t *eras = a.eras ? a.eras + k * a.eras_stride : nullptr;
     const unsigned ne = a.neras ? a.neras[k] : 0;
     uint32_t *pos = a.positions ? a.positions + k * a.pos_stride : nullptr;
     T *corr = a.corr ? static_cast<T *>(a.corr) + k * a.corr_stride : nullptr;
     if constexpr (MAXR <= 32) {        // working arrays in LDS, lanes interleaved (kDecBlock lanes)
         __shared__ uint16_t work[kWorkArrays<MAXR> * (MAXR + 1) * kDecBlock];
-        a.result[k] = decode_one<T, MAXR, kDecBlock>(c, A, I, ID, FD, data, a.len, parity, eras, ne,
+        a.result[k] = decode_one<T, MAXR, kDecBlock>(c, A, I, ID, FD, data, len, parity, eras, ne,
                                                      pos, corr, static_cast<const uint8_t *>(nullptr), work + threadIdx.x);
     } else {
-        a.result[k] = decode_one<T, MAXR>(c, A, I, ID, FD, data, a.len, parity, eras, ne, pos, corr);
+        a.result[k] = decode_one<T, MAXR>(c, A, I, ID, FD, data, len, parity, eras, ne, pos, corr);
     }
 }
 

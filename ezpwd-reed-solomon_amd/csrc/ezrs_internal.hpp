@@ -35,6 +35,28 @@ struct DevCodec {
     const uint8_t *from_dual;     // device, 256
 };
 
+// Shard batches (ezrs_encode_shards / ezrs_decode_shards): codeword k is row j = k mod rows of
+// shard s = k / rows, at element offset s * pitch + j * stride; every row holds `len` data symbols
+// and its parity, except the shard's last row, which holds `tail` data symbols (a shortened
+// codeword) and its parity.  rows == 0: a plain batch (row k at k * stride).
+struct Shards {
+    uint32_t rows = 0;
+    uint32_t tail = 0;
+    size_t pitch = 0;
+};
+
+// Element offset and data length of row k.
+__host__ __device__ __forceinline__ size_t shard_row(const Shards &g, size_t k, size_t stride, unsigned len,
+                                                     unsigned &rlen) {
+    if (!g.rows) {
+        rlen = len;
+        return k * stride;
+    }
+    const size_t s = k / g.rows, j = k - s * g.rows;
+    rlen = j + 1 == g.rows ? g.tail : len;
+    return s * g.pitch + j * stride;
+}
+
 // Arguments of one batch decode (strides in elements).
 struct DecodeArgs {
     void *data;
@@ -51,6 +73,7 @@ struct DecodeArgs {
     void *corr;
     size_t corr_stride;
     size_t ncw;
+    Shards sh{};                  // sh.rows != 0: shard rows, parity inline (data + row length)
 };
 
 struct EncodeArgs {
@@ -60,7 +83,23 @@ struct EncodeArgs {
     void *parity;
     size_t parity_stride;
     size_t ncw;
+    Shards sh{};                  // sh.rows != 0: shard rows, parity inline (data + row length)
 };
+
+// Row k's data and parity pointers and data length (plain batches: the strided arrays; shard
+// batches: the row, its parity right after its data).
+template <typename T, typename P, class A>
+__host__ __device__ __forceinline__ void row_ptrs(const A &a, size_t k, P *&data, T *&parity, unsigned &len) {
+    if (!a.sh.rows) {
+        len = a.len;
+        data = static_cast<P *>(a.data) + k * a.data_stride;
+        parity = static_cast<T *>(a.parity) + k * a.parity_stride;
+        return;
+    }
+    const size_t off = shard_row(a.sh, k, a.data_stride, a.len, len);
+    data = static_cast<P *>(a.data) + off;
+    parity = const_cast<T *>(reinterpret_cast<const T *>(data)) + len;
+}
 
 // Generic per-codeword kernels (ezrs_generic.hip): every codec, every length.
 hipError_t launch_encode_generic(const DevCodec &c, const EncodeArgs &a, hipStream_t s);

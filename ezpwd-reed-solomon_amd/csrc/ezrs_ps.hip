@@ -80,6 +80,9 @@ struct PsArgs {
     uint8_t *parity;            // tile encode: parity of codeword k at parity + k * pstride
     uint32_t pstride;
     uint32_t pspan;             // bytes writable from parity
+    uint32_t srows;             // shard batches (Shards): codewords per shard, 0 = a plain batch
+    int stail_lo;               // full-frame position of a shard's last row's first byte
+    uint32_t spitch;            // shard pitch in bytes
     int ablate;                 // timing experiments only (tools/pt_ablate.py, EZRS_PT_ABLATE): bit 0
                                 // no main loop, 1 no exchange, 2 no fold, 3 no DMA, 5 nothing flagged
 };
@@ -440,8 +443,9 @@ constexpr int kLds = 81920;                   // 80 KiB: two workgroups per CU
 constexpr int kGuard = 256;                   // bytes before the image: row 0's pad positions
 constexpr int kImage = 65536;                 // the tile image (256 rows x pitch <= 256 B)
 constexpr int kFlags = kGuard + kImage;       // decode flags [8][64] after the image
+constexpr int kTab = kFlags + 2048;           // shard batches: per-row image offset and pad [256]
 constexpr uint32_t kOob = 0xF0000000u;        // a buffer offset past every span (ps_max_rows)
-static_assert(kFlags + 2048 <= kLds, "tile kernel LDS");
+static_assert(kTab + 1024 <= kLds, "tile kernel LDS");
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
@@ -521,6 +525,14 @@ __device__ __forceinline__ void exchange(uint32_t (&V)[C::NI][8], uint32_t lx) {
 // One tile buffer per workgroup; the other workgroup on the CU computes while this one's next tile
 // lands.  The exchange uses the whole 80 KiB once the image is consumed.
 
+// Shard batches: byte offset (from the span base) and pad (full-frame position of the first byte)
+// of codeword k.  Row j of shard q sits at q * spitch + j * stride; a shard's last row is shortened.
+__device__ __forceinline__ uint32_t row_at(const PsArgs &a, uint32_t k, int &lo) {
+    const uint32_t q = k / a.srows, j = k - q * a.srows;
+    lo = j + 1 == a.srows ? a.stail_lo : a.lo;
+    return q * a.spitch + j * a.stride;
+}
+
 __device__ __forceinline__ void issue_tile_lin(uint32_t lbuf, pw_rsrc_t rsrc, uint32_t toff, uint32_t tile_bytes,
                                                int w, int ablate) {
     if (ablate & 8) return;
@@ -574,10 +586,52 @@ __device__ __forceinline__ void read_rows_lin(u32x4 (&R)[4], uint32_t lbuf, uint
     }
 }
 
-template <class C, int G, int HI>
+// Shard batches: rows 4l + k from their row-table entries e (image offset of position 0 | pad << 24,
+// written at the tile's start); in the pieces below the shortened rows' pad (pa < tail_lo, only in
+// tiles that hold a shortened row) the bytes before each row's own pad -- the previous row's, in
+// the linear image -- are masked off.
+__device__ __forceinline__ void read_rows_shard(u32x4 (&R)[4], uint32_t lbuf, int pa, int tail_lo, const u32x4 &e) {
+    u32x2 d2[4][2];
+    uint32_t d4[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t at = (lbuf + (e[k] & 0xFFFFFFu) + (uint32_t)pa) & ~3u;
+        asm volatile("ds_read2_b32 %0, %3 offset1:1\n\t"
+                     "ds_read2_b32 %1, %3 offset0:2 offset1:3\n\t"
+                     "ds_read_b32 %2, %3 offset:16"
+                     : "=&v"(d2[k][0]), "=&v"(d2[k][1]), "=&v"(d4[k]) : "v"(at) : "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(d2[0][0]), "+v"(d2[0][1]), "+v"(d4[0]), "+v"(d2[1][0]), "+v"(d2[1][1]), "+v"(d4[1]),
+                   "+v"(d2[2][0]), "+v"(d2[2][1]), "+v"(d4[2]), "+v"(d2[3][0]), "+v"(d2[3][1]), "+v"(d4[3])
+                 :: "memory");
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t d[5] = {d2[k][0].x, d2[k][0].y, d2[k][1].x, d2[k][1].y, d4[k]};
+        const uint32_t sh = lbuf + (e[k] & 0xFFFFFFu) + (uint32_t)pa;      // byte phase in bits 0..1
+#pragma unroll
+        for (int j = 0; j < 4; ++j) R[k][j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
+    }
+    if (pa < tail_lo) {                                      // wave-uniform
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int z8 = 8 * ((int)(e[k] >> 24) - pa);     // pad bits at the piece's start
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int c = min(max(z8 - 32 * j, 0), 32);
+                R[k][j] &= (uint32_t)(0xFFFFFFFFull << c);
+            }
+        }
+    }
+}
+
+template <class C, int G, int HI, bool SH>
 __device__ __forceinline__ void lin_pass(uint32_t (&V)[C::NI][8], uint32_t lbuf, uint32_t stride, int q, int lo,
-                                         const uint32_t (&ph)[4]) {
+                                         const uint32_t (&ph)[4], int tail_lo) {
     constexpr int NP = C::NP0[G] + C::NP1[G];
+    u32x4 e = {0, 0, 0, 0};
+    if constexpr (SH)
+        asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(e) : "v"(lbuf + kTab + 16u * fresh()) : "memory");
     static_for<0, NP>([&](auto Ic) {
         constexpr int I = decltype(Ic)::value;
         constexpr int p0 = C::PIECE[G][I];
@@ -585,7 +639,8 @@ __device__ __forceinline__ void lin_pass(uint32_t (&V)[C::NI][8], uint32_t lbuf,
             const int pa = 16 * (p0 + q);
             if (pa < HI) {                                   // wave-uniform
                 u32x4 R[4];
-                read_rows_lin(R, lbuf, stride, pa, lo, ph);
+                if constexpr (SH) read_rows_shard(R, lbuf, pa, tail_lo, e);
+                else read_rows_lin(R, lbuf, stride, pa, lo, ph);
                 uint32_t X[8];
                 {
                     const uint32_t c0[4] = {R[0].x, R[1].x, R[2].x, R[3].x};
@@ -609,7 +664,7 @@ __device__ __forceinline__ void lin_pass(uint32_t (&V)[C::NI][8], uint32_t lbuf,
 // Fix-up, exchange (through the consumed image), next tile's DMA, fold and stores of wave W.
 template <class C, bool ENC, int W>
 __device__ __forceinline__ void wave_tail_lin(uint32_t (&V)[C::NI][8], const PsArgs &a, uint32_t lbuf,
-                                              uint32_t tile, uint32_t noff, uint32_t tile_bytes,
+                                              uint32_t tile, uint32_t noff, uint32_t nbytes,
                                               pw_rsrc_t rsrc, pw_rsrc_t rout, pw_rsrc_t rws, int pt_it = 0) {
     const int pt_w = W;
     (void)pt_it; (void)pt_w;
@@ -619,7 +674,7 @@ __device__ __forceinline__ void wave_tail_lin(uint32_t (&V)[C::NI][8], const PsA
         exchange<C, W, 0>(V, lbuf + 16u * fresh());         // slot (W XCAP + j) at 2 KiB each
     }
     PT_STAMP(4);
-    if (noff != kOob) issue_tile_lin(lbuf, rsrc, noff, tile_bytes, W, a.ablate);
+    if (noff != kOob) issue_tile_lin(lbuf, rsrc, noff, nbytes, W, a.ablate);
     uint32_t T[C::NOWN][8];
 #pragma unroll
     for (int i = 0; i < C::NOWN; ++i)
@@ -688,16 +743,29 @@ __device__ __forceinline__ void wave_tail_lin(uint32_t (&V)[C::NI][8], const PsA
     PT_STAMP(6);
 }
 
-template <class C, bool ENC, int G>
+template <class C, bool ENC, int G, bool SH>
 __device__ __forceinline__ void pt_run_lin(const PsArgs &a, uint8_t *lds, int w) {
     constexpr int HI = ENC ? kN - (int)C::NR : kN;
     const pw_rsrc_t rsrc = pw_rsrc(a.base, a.span);
     const uint32_t lbuf = __builtin_amdgcn_readfirstlane(lds_addr(lds));
-    const uint32_t tile_bytes = a.stride * kTile;
     const pw_rsrc_t rout = pw_rsrc(reinterpret_cast<const uint8_t *>(a.result), ENC ? 0u : a.ncw * 4u);
     const pw_rsrc_t rws = pw_rsrc(a.ws, ENC ? (uint32_t)(C::NR * a.ws_pitch) : a.ncw * 32u);
+    constexpr bool shards = SH;
+    // byte range of tile t: plain batches t * 256 rows of pitch stride; shard batches from its first
+    // row's start to the next tile's (the span's end for the last tile)
+    auto tile_range = [&](uint32_t t, uint32_t &bytes) -> uint32_t {
+        if (!shards) {
+            bytes = a.stride * kTile;
+            return t * bytes;
+        }
+        int lo;
+        const uint32_t t0 = t * kTile, off = row_at(a, t0, lo);
+        bytes = (t0 + kTile < a.ncw ? row_at(a, t0 + kTile, lo) : a.span) - off;
+        return off;
+    };
     uint32_t tile = blockIdx.x;
-    issue_tile_lin(lbuf, rsrc, tile * tile_bytes, tile_bytes, w, a.ablate);
+    uint32_t tbytes, toff = tile < a.ntiles ? tile_range(tile, tbytes) : 0u;
+    if (tile < a.ntiles) issue_tile_lin(lbuf, rsrc, toff, tbytes, w, a.ablate);
     int pt_it = 0, pt_w = w;
     (void)pt_it; (void)pt_w;
     for (; tile < a.ntiles; tile += gridDim.x, ++pt_it) {
@@ -707,8 +775,8 @@ __device__ __forceinline__ void pt_run_lin(const PsArgs &a, uint8_t *lds, int w)
         uint32_t ph[4];                                      // byte phase of row k's start
 #pragma unroll
         for (int k = 0; k < 4; ++k) ph[k] = (lbuf + kGuard + k * a.stride - (uint32_t)lo) & 3u;
-        const uint32_t toff = tile * tile_bytes;
-        const uint32_t noff = tile + gridDim.x < a.ntiles ? toff + gridDim.x * tile_bytes : kOob;
+        uint32_t nbytes = 0;
+        const uint32_t noff = tile + gridDim.x < a.ntiles ? tile_range(tile + gridDim.x, nbytes) : kOob;
         uint32_t V[C::NI][8];
 #pragma unroll
         for (int s = 0; s < C::NI; ++s)
@@ -716,9 +784,22 @@ __device__ __forceinline__ void pt_run_lin(const PsArgs &a, uint8_t *lds, int w)
             for (int t = 0; t < 8; ++t) V[s][t] = 0;
         PT_STAMP(0);
         wait_vm<0>();                                        // the tile landed (and the stores went)
+        if constexpr (SH) {                                  // row table: wave w writes rows 32w ..
+            const uint32_t j = fresh();
+            if (j < 32u) {
+                const uint32_t r = 32u * (uint32_t)w + j, k = tile * kTile + r;
+                uint32_t e = kGuard;
+                if (k < a.ncw) {
+                    int rlo;
+                    const uint32_t at = row_at(a, k, rlo);
+                    e = (kGuard + at - toff - (uint32_t)rlo) | ((uint32_t)rlo << 24);
+                }
+                asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" :: "v"(lbuf + kTab + 4u * r), "v"(e) : "memory");
+            }
+        }
         barrier();
         PT_STAMP(1);
-        if (toff + tile_bytes > a.span) {                    // last tile: the span's final bytes
+        if (toff + tbytes >= a.span) {                       // last tile: the span's final bytes
             // a 16-byte DMA piece that crosses the span's end comes back all-zero: re-read the last
             // 64 bytes one by one (out-of-range bytes read as zero)
             if (w == 0) {
@@ -737,7 +818,12 @@ __device__ __forceinline__ void pt_run_lin(const PsArgs &a, uint8_t *lds, int w)
         if (EZRS_PT_PRIO == 1 && w >= 4) asm volatile("s_setprio 1");
         if (EZRS_PT_PRIO == 2) { if (w >= 6) asm volatile("s_setprio 3"); else if (w >= 4) asm volatile("s_setprio 2"); else if (w >= 2) asm volatile("s_setprio 1"); }
 #endif
-        if (!(a.ablate & 1)) lin_pass<C, G, HI>(V, lbuf, a.stride, q, lo, ph);
+        int tlo = lo;                                        // shard batches: pad of the tile's rows
+        if constexpr (SH) {
+            const uint32_t t0 = tile * kTile, kt = (t0 / a.srows) * a.srows + a.srows - 1;
+            if (kt < t0 + kTile && kt < a.ncw) tlo = a.stail_lo;
+        }
+        if (!(a.ablate & 1)) lin_pass<C, G, HI, SH>(V, lbuf, a.stride, q, lo, ph, tlo);
 #if EZRS_PT_PRIO
         asm volatile("s_setprio 0");
 #endif
@@ -745,20 +831,22 @@ __device__ __forceinline__ void pt_run_lin(const PsArgs &a, uint8_t *lds, int w)
         barrier();                                           // the image is consumed
         PT_STAMP(3);
         switch (w / C::GN) {
-        case 0: wave_tail_lin<C, ENC, G>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws, pt_it); break;
-        case 1: if constexpr (C::QN > 1) wave_tail_lin<C, ENC, G + C::GN>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws, pt_it); break;
-        case 2: if constexpr (C::QN > 2) wave_tail_lin<C, ENC, G + 2 * C::GN>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws, pt_it); break;
-        case 3: if constexpr (C::QN > 3) wave_tail_lin<C, ENC, G + 3 * C::GN>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws, pt_it); break;
-        case 4: if constexpr (C::QN > 4) wave_tail_lin<C, ENC, G + 4 * C::GN>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws, pt_it); break;
-        case 5: if constexpr (C::QN > 5) wave_tail_lin<C, ENC, G + 5 * C::GN>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws, pt_it); break;
-        case 6: if constexpr (C::QN > 6) wave_tail_lin<C, ENC, G + 6 * C::GN>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws, pt_it); break;
-        default: if constexpr (C::QN > 7) wave_tail_lin<C, ENC, G + 7 * C::GN>(V, a, lbuf, tile, noff, tile_bytes, rsrc, rout, rws, pt_it); break;
+        case 0: wave_tail_lin<C, ENC, G>(V, a, lbuf, tile, noff, nbytes, rsrc, rout, rws, pt_it); break;
+        case 1: if constexpr (C::QN > 1) wave_tail_lin<C, ENC, G + C::GN>(V, a, lbuf, tile, noff, nbytes, rsrc, rout, rws, pt_it); break;
+        case 2: if constexpr (C::QN > 2) wave_tail_lin<C, ENC, G + 2 * C::GN>(V, a, lbuf, tile, noff, nbytes, rsrc, rout, rws, pt_it); break;
+        case 3: if constexpr (C::QN > 3) wave_tail_lin<C, ENC, G + 3 * C::GN>(V, a, lbuf, tile, noff, nbytes, rsrc, rout, rws, pt_it); break;
+        case 4: if constexpr (C::QN > 4) wave_tail_lin<C, ENC, G + 4 * C::GN>(V, a, lbuf, tile, noff, nbytes, rsrc, rout, rws, pt_it); break;
+        case 5: if constexpr (C::QN > 5) wave_tail_lin<C, ENC, G + 5 * C::GN>(V, a, lbuf, tile, noff, nbytes, rsrc, rout, rws, pt_it); break;
+        case 6: if constexpr (C::QN > 6) wave_tail_lin<C, ENC, G + 6 * C::GN>(V, a, lbuf, tile, noff, nbytes, rsrc, rout, rws, pt_it); break;
+        default: if constexpr (C::QN > 7) wave_tail_lin<C, ENC, G + 7 * C::GN>(V, a, lbuf, tile, noff, nbytes, rsrc, rout, rws, pt_it); break;
         }
+        toff = noff;
+        tbytes = nbytes;
     }
     wait_vm<0>();                                            // no DMA may land after the exit
 }
 
-template <class C, bool ENC>
+template <class C, bool ENC, bool SH>
 __global__ void __attribute__((amdgpu_flat_work_group_size(kThreads, kThreads), amdgpu_waves_per_eu(4)))
 k_pt_lin(PsArgs a) {
     static_assert(C::NQ == 1, "one quad (4 syndromes) per wave");
@@ -766,8 +854,8 @@ k_pt_lin(PsArgs a) {
     static_assert(8 * C::XCAP * 2048 <= kLds, "exchange area");
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLds];
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (C::GN == 1 || w % C::GN == 0) pt_run_lin<C, ENC, 0>(a, lds, w);
-    else pt_run_lin<C, ENC, C::GN - 1>(a, lds, w);
+    if (C::GN == 1 || w % C::GN == 0) pt_run_lin<C, ENC, 0, SH>(a, lds, w);
+    else pt_run_lin<C, ENC, C::GN - 1, SH>(a, lds, w);
 }
 
 } // namespace pt
@@ -788,7 +876,7 @@ constexpr int kParCw = 32 * kParGroups;
 // wave's share of the map and doubling the waves that hide the phases' latencies.
 template <class C, bool PERM>
 __global__ void __launch_bounds__(512) k_ps_parity8(const uint8_t *ws, size_t ws_pitch, uint8_t *parity,
-                                                    size_t pstride, size_t ncw) {
+                                                    size_t pstride, size_t ncw, Shards sh, unsigned len) {
     constexpr int NR = C::NR;
     constexpr int kRegion = 32 * NR + 8;                       // bytes per group in the stage
     constexpr int kPlanes = 8 * NR * kParGroups;               // dwords
@@ -844,7 +932,9 @@ __global__ void __launch_bounds__(512) k_ps_parity8(const uint8_t *ws, size_t ws
         const size_t x = cwb + r;
         const size_t k = PERM ? ((x & ~(size_t)255) | ((x & 3) << 6) | ((x >> 2) & 63)) : x;
         if (k >= ncw) continue;
-        uint8_t *dst = parity + k * pstride;
+        unsigned rlen;
+        // shard batches: parity is the base of the rows, each row's parity after its data
+        uint8_t *dst = sh.rows ? parity + shard_row(sh, k, pstride, len, rlen) + rlen : parity + k * pstride;
         const uint8_t *s8 = stage + (r >> 5) * kRegion + (r & 31) * NR;
         if constexpr (NR % 8 == 0) {
 #pragma unroll
@@ -928,30 +1018,53 @@ size_t ps_ws_bytes(size_t ncw) { return ps_pitch(ncw) * 32; }
 // the tile kernel's out-of-range marker kOob is above them).
 static size_t ps_max_rows(size_t stride) { return ((size_t)0xE0000000u / stride) / 2048 * 2048; }
 
+// Shard batches: rows per launch, whole shards (byte offsets stay below 0xE0000000 as above).
+static size_t ps_max_rows_shards(const Shards &g) {
+    const size_t n = (size_t)0xE0000000u / g.pitch;
+    return (n ? n : 1) * g.rows;
+}
+
+// Shard batches: a tile's rows must fit the 64 KiB image (no gaps between shards beyond a row's
+// width) and every launch's span the 32-bit offsets.
+static bool ps_shards_ok(const Shards &g, size_t stride) {
+    return g.pitch <= (size_t)g.rows * stride && g.pitch < 0xE0000000u;
+}
+
 bool ps_can_encode(const DevCodec &, const EncodeArgs &a) {
+    if (a.sh.rows) return a.data_stride <= 256 && ps_variant() == 0 && ps_shards_ok(a.sh, a.data_stride);
     return a.data_stride >= 1 && a.data_stride <= 256;
 }
 
 bool ps_can_decode(const DevCodec &d, const DecodeArgs &a) {
+    if (a.sh.rows) return a.data_stride <= 256 && ps_variant() == 0 && ps_shards_ok(a.sh, a.data_stride);
     const bool inline_par = a.parity == static_cast<char *>(a.data) + a.len && a.parity_stride == a.data_stride;
     return inline_par && a.data_stride <= 256 && a.data_stride >= a.len + d.nroots;
 }
 
 hipError_t launch_ps_encode(int id, const DevCodec &d, const EncodeArgs &a, void *ws, hipStream_t s) {
     const size_t pitch = a.data_stride > a.parity_stride ? a.data_stride : a.parity_stride;
-    const size_t maxr = ps_max_rows(pitch);
+    const size_t maxr = a.sh.rows ? ps_max_rows_shards(a.sh) : ps_max_rows(pitch);
     const int var = ps_variant();
     for (size_t k0 = 0; k0 < a.ncw; k0 += maxr) {
         const size_t n = a.ncw - k0 < maxr ? a.ncw - k0 : maxr;
         ps::PsArgs p{};
-        p.base = static_cast<const uint8_t *>(a.data) + k0 * a.data_stride;
-        p.span = (uint32_t)((n - 1) * a.data_stride + a.len);
+        unsigned rlen;
+        const size_t b0 = shard_row(a.sh, k0, a.data_stride, a.len, rlen);   // chunks start a shard
+        const size_t last = shard_row(a.sh, n - 1, a.data_stride, a.len, rlen);
+        p.base = static_cast<const uint8_t *>(a.data) + b0;
+        p.span = (uint32_t)(last + rlen);
         p.stride = (uint32_t)a.data_stride;
+        if (a.sh.rows) {
+            p.srows = a.sh.rows;
+            p.stail_lo = (int)(d.load - a.sh.tail);
+            p.spitch = (uint32_t)a.sh.pitch;
+        }
         p.ncw = (uint32_t)n;
         p.ntiles = (uint32_t)((n + ps::kTile - 1) / ps::kTile);
         p.lo = (int)(d.load - a.len);              // leading zero positions of a shortened code
         p.hi = (int)d.load;                        // data positions only
-        uint8_t *par = static_cast<uint8_t *>(a.parity) + k0 * a.parity_stride;
+        // shard batches: the parity kernel finds each row's parity from the rows' base
+        uint8_t *par = a.sh.rows ? const_cast<uint8_t *>(p.base) : static_cast<uint8_t *>(a.parity) + k0 * a.parity_stride;
         p.parity = par;
         p.pstride = (uint32_t)a.parity_stride;
         p.pspan = (uint32_t)((n - 1) * a.parity_stride + d.nroots);
@@ -964,14 +1077,20 @@ hipError_t launch_ps_encode(int id, const DevCodec &d, const EncodeArgs &a, void
         if (k++ == id) {                                                                          \
             const unsigned pgrid = (unsigned)((n + ps::kParCw - 1) / ps::kParCw);                 \
             if (var == 0) {                                                                       \
-                hipLaunchKernelGGL((ps::pt::k_pt_lin<ps::PT_##C, true>), dim3(grid), dim3(ps::pt::kThreads), \
-                                   0, s, p);                                                      \
+                if (a.sh.rows)                                                                    \
+                    hipLaunchKernelGGL((ps::pt::k_pt_lin<ps::PT_##C, true, true>), dim3(grid),    \
+                                       dim3(ps::pt::kThreads), 0, s, p);                          \
+                else                                                                              \
+                    hipLaunchKernelGGL((ps::pt::k_pt_lin<ps::PT_##C, true, false>), dim3(grid),   \
+                                       dim3(ps::pt::kThreads), 0, s, p);                          \
                 hipLaunchKernelGGL((ps::k_ps_parity8<ps::PS_##C, false>), dim3(pgrid), dim3(512), 0, s, \
-                                   static_cast<const uint8_t *>(ws), p.ws_pitch, par, a.parity_stride, n); \
+                                   static_cast<const uint8_t *>(ws), p.ws_pitch, par, a.parity_stride, n, \
+                                   a.sh, a.len);                                                  \
             } else {                                                                              \
                 hipLaunchKernelGGL((ps::k_py_syndromes<ps::PY_##C, true>), dim3(grid), dim3(128), 0, s, p); \
                 hipLaunchKernelGGL((ps::k_ps_parity8<ps::PS_##C, true>), dim3(pgrid), dim3(512), 0, s, \
-                                   static_cast<const uint8_t *>(ws), p.ws_pitch, par, a.parity_stride, n); \
+                                   static_cast<const uint8_t *>(ws), p.ws_pitch, par, a.parity_stride, n, \
+                                   Shards{}, a.len);                                              \
             }                                                                                     \
         }
         EZRS_PS_CODEC_LIST(EZRS_PS_ENC)
@@ -984,14 +1103,22 @@ hipError_t launch_ps_encode(int id, const DevCodec &d, const EncodeArgs &a, void
 
 hipError_t launch_ps_syndromes(int id, const DevCodec &d, const DecodeArgs &a, uint8_t *syn_ws,
                                hipStream_t s) {
-    const size_t maxr = ps_max_rows(a.data_stride);
+    const size_t maxr = a.sh.rows ? ps_max_rows_shards(a.sh) : ps_max_rows(a.data_stride);
     const int var = ps_variant();
     for (size_t k0 = 0; k0 < a.ncw; k0 += maxr) {
         const size_t n = a.ncw - k0 < maxr ? a.ncw - k0 : maxr;
         ps::PsArgs p{};
-        p.base = static_cast<const uint8_t *>(a.data) + k0 * a.data_stride;
-        p.span = (uint32_t)((n - 1) * a.data_stride + a.len + d.nroots);
+        unsigned rlen;
+        const size_t b0 = shard_row(a.sh, k0, a.data_stride, a.len, rlen);   // chunks start a shard
+        const size_t last = shard_row(a.sh, n - 1, a.data_stride, a.len, rlen);
+        p.base = static_cast<const uint8_t *>(a.data) + b0;
+        p.span = (uint32_t)(last + rlen + d.nroots);
         p.stride = (uint32_t)a.data_stride;
+        if (a.sh.rows) {
+            p.srows = a.sh.rows;
+            p.stail_lo = (int)(d.load - a.sh.tail);
+            p.spitch = (uint32_t)a.sh.pitch;
+        }
         p.ncw = (uint32_t)n;
         p.ntiles = (uint32_t)((n + ps::kTile - 1) / ps::kTile);
         p.lo = (int)(d.load - a.len);
@@ -1006,9 +1133,12 @@ hipError_t launch_ps_syndromes(int id, const DevCodec &d, const DecodeArgs &a, u
         int k = 0;
 #define EZRS_PS_SYN(C)                                                                            \
         if (k++ == id) {                                                                          \
-            if (var == 0)                                                                         \
-                hipLaunchKernelGGL((ps::pt::k_pt_lin<ps::PT_##C, false>), dim3(grid), dim3(ps::pt::kThreads), \
-                                   0, s, p);                                                      \
+            if (var == 0 && a.sh.rows)                                                            \
+                hipLaunchKernelGGL((ps::pt::k_pt_lin<ps::PT_##C, false, true>), dim3(grid),       \
+                                   dim3(ps::pt::kThreads), 0, s, p);                              \
+            else if (var == 0)                                                                    \
+                hipLaunchKernelGGL((ps::pt::k_pt_lin<ps::PT_##C, false, false>), dim3(grid),      \
+                                   dim3(ps::pt::kThreads), 0, s, p);                              \
             else                                                                                  \
                 hipLaunchKernelGGL((ps::k_py_syndromes<ps::PY_##C, false>), dim3(grid), dim3(128), 0, s, p); \
         }

@@ -83,6 +83,13 @@ def lib():
         L.ezrs_stream_encode.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, C.POINTER(_sz)]
         L.ezrs_stream_decode.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, C.POINTER(_sz),
                                          C.POINTER(_sz)]
+        L.ezrs_shard_codewords.restype = _sz
+        L.ezrs_shard_codewords.argtypes = [_vp, _sz, _u]
+        L.ezrs_shard_encoded_len.restype = _sz
+        L.ezrs_shard_encoded_len.argtypes = [_vp, _sz, _u]
+        L.ezrs_encode_shards.argtypes = [_vp, _vp, _sz, _sz, _u, _sz, _vp]
+        L.ezrs_decode_shards.argtypes = [_vp, _vp, _sz, _sz, _u, _sz, _vp, _sz, _vp, _vp, _vp, _sz,
+                                         _vp, _sz, _vp]
         L.ezrs_host_alloc.argtypes = [C.POINTER(_vp), _sz]
         L.ezrs_host_free.argtypes = [_vp]
         L.ezbch_last_error.restype = C.c_char_p
@@ -255,6 +262,44 @@ class Codec:
             self._h, _tp(data), ds, length, _tp(parity), ps, _tp(eras), es, _tp(neras),
             _tp(result), _tp(positions), qs, _tp(corr), cs, ncw, _stream_ptr(stream)),
             "ezrs_decode")
+        return result
+
+    # -- shard batches (rsencode layout per shard) --------------------------------------------
+    def shard_codewords(self, shard_len, chunk=None):
+        """Codewords per shard of shard_len data symbols cut into chunks (default: the load)."""
+        return int(lib().ezrs_shard_codewords(self._h, shard_len, chunk or self.load))
+
+    def shard_encoded_len(self, shard_len, chunk=None):
+        return int(lib().ezrs_shard_encoded_len(self._h, shard_len, chunk or self.load))
+
+    def encode_shards(self, shards, shard_len, chunk=None, stream=None):
+        """shards: [nshards, pitch] device tensor, each row one shard in the rsencode layout
+        (chunks of `chunk` data symbols, each followed by its parity; the last chunk shorter);
+        writes every codeword's parity (ezrs_encode_shards)."""
+        w = self.info.datum_bytes
+        sp = _dev_rows(shards, "shards", self.device, w)
+        _check(lib().ezrs_encode_shards(self._h, _tp(shards), sp, shard_len, chunk or self.load,
+                                        shards.shape[0], _stream_ptr(stream)), "ezrs_encode_shards")
+
+    def decode_shards(self, shards, shard_len, chunk=None, eras=None, neras=None, result=None,
+                      positions=None, corr=None, stream=None):
+        """In-place decode of every codeword of every shard; returns the int32 result tensor
+        [nshards * codewords per shard] (shard-major)."""
+        import torch
+        w = self.info.datum_bytes
+        chunk = chunk or self.load
+        sp = _dev_rows(shards, "shards", self.device, w)
+        es = _dev_rows(eras, "eras", self.device, 4)
+        _dev_rows(neras, "neras", self.device, 4, ndim=1)
+        qs = _dev_rows(positions, "positions", self.device, 4)
+        cs = _dev_rows(corr, "corr", self.device, w)
+        ncw = shards.shape[0] * self.shard_codewords(shard_len, chunk)
+        if result is None:
+            result = torch.empty(ncw, dtype=torch.int32, device=shards.device)
+        _dev_rows(result, "result", self.device, 4, ndim=1)
+        _check(lib().ezrs_decode_shards(
+            self._h, _tp(shards), sp, shard_len, chunk, shards.shape[0], _tp(eras), es, _tp(neras),
+            _tp(result), _tp(positions), qs, _tp(corr), cs, _stream_ptr(stream)), "ezrs_decode_shards")
         return result
 
     # -- host batch forms ----------------------------------------------------------------------

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define EZRS_ABI_VERSION 4
+#define EZRS_ABI_VERSION 5
 
 typedef struct ezrs_codec ezrs_codec;
 
@@ -129,6 +129,25 @@ int ezrs_decode_ws(const ezrs_codec *codec, void *data, size_t data_stride, unsi
                    const uint32_t *neras, int32_t *result, uint32_t *positions, size_t pos_stride,
                    void *corr, size_t corr_stride, size_t ncw, void *ws, size_t ws_bytes,
                    void *stream);
+
+/* Shard batches (device-resident).  A shard of `shard_len` data symbols is stored as the rsencode
+ * wire format lays it out (rsencode.C:93-163, one encode/decode per chunk): R = ceil(shard_len /
+ * chunk) codewords back to back, each `chunk` data symbols followed by its NROOTS parity symbols,
+ * except the last, which carries the remaining shard_len - (R-1)*chunk data symbols (a shortened
+ * codeword, rs_base:1302-1304) and its parity.  Shard i starts at shards + i*shard_pitch (elements,
+ * >= ezrs_shard_encoded_len).  Codewords are numbered shard-major, k = i*R + j: result[k],
+ * erasure / position / correction rows k are codeword j of shard i, positions relative to that
+ * codeword's first data symbol.  The whole batch is one launch of the codec's kernels. */
+size_t ezrs_shard_codewords(const ezrs_codec *codec, size_t shard_len, unsigned chunk);
+size_t ezrs_shard_encoded_len(const ezrs_codec *codec, size_t shard_len, unsigned chunk);
+/* Writes every codeword's parity (its data is only read). */
+int ezrs_encode_shards(const ezrs_codec *codec, void *shards, size_t shard_pitch, size_t shard_len,
+                       unsigned chunk, size_t nshards, void *stream);
+/* Decodes every codeword in place: result[k] etc. as ezrs_decode, for nshards * R codewords. */
+int ezrs_decode_shards(const ezrs_codec *codec, void *shards, size_t shard_pitch, size_t shard_len,
+                       unsigned chunk, size_t nshards, const uint32_t *eras, size_t eras_stride,
+                       const uint32_t *neras, int32_t *result, uint32_t *positions,
+                       size_t pos_stride, void *corr, size_t corr_stride, void *stream);
 
 /* Host-memory forms: the same contracts with HOST pointers.  The batch is streamed through the
  * device in chunks of `chunk` codewords (0 = library default) over two HIP streams with

@@ -22,7 +22,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert ezrs.lib().ezrs_abi_version() == 4
+    assert ezrs.lib().ezrs_abi_version() == 5
 
 
 def test_invalid_codecs_rejected_before_device():
