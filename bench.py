@@ -553,6 +553,9 @@ def main():
                          "RS(255,223) 8 errors + 4 erasures decode; c4: RS(65535,65503); c5: "
                          "BCH(1023,983,4) (SURVEY.md 8d); shards: RS(255,223) over S-byte shards, "
                          "S = 1 KiB .. 1 MiB (rsencode layout, one call per direction)")
+    ap.add_argument("--k", type=int, default=0,
+                    help="c2 workload with another RS(255,K) codec (the plane-sliced set: "
+                         "NROOTS <= 32); the headline is K = 223")
     ap.add_argument("--harness-check", action="store_true",
                     help="CPU/gloo check of the multi-rank harness (placeholder step, no GPU)")
     args = ap.parse_args()
@@ -581,7 +584,7 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    n, k = (255, 251) if args.workload == "c1" else (N, K)
+    n, k = (255, 251) if args.workload == "c1" else (N, args.k or K)
     enc_bytes, dec_bytes = n, n + 4               # encode: k read + n-k written; decode: n read + result
     codec = ezrs.Codec.rs(n, k, device=local)
     ncw = args.ncw

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Generate the plane-sliced GF(2^8) RS syndrome kernels' constant code (csrc/gen/ezrs_ps_tables.inc).
+"""Generate the plane-sliced GF(2^8) RS kernels' constant code (csrc/gen/ezrs_ps_tables.inc).
 
 Word layout.  A 32-bit word holds ONE position of FOUR codewords: byte k = the symbol of codeword
 k, so bit 8k + b is bit-plane b of codeword k.  Every bit of the word is an independent GF(2)
@@ -12,23 +12,20 @@ Plane slicing.  With r_p = sum_b bit_b(r_p) alpha^b (polynomial basis), a syndro
 
 and, because the V's coefficients are bits, V_{b,2e} = V_{b,e}^2.  So only one root per
 cyclotomic coset ("leader") is evaluated in the main loop -- 16 of the 32 roots of RS(255,223) --
-and the others follow by squaring in the epilogue: the main loop's state is 8 GF(2^8) bits per
-leader, 128 words for RS(255,223), half of what a per-symbol bit-slicing of 32 syndromes needs.
+and the others follow by squaring in the epilogue.
 
-Main loop.  Per 8 positions and leader bit q the state word takes one 3-input XOR of two
-Four-Russians combinations (all 15 XORs of four position words are formed once per 4 positions).
-A workgroup of 8 waves covers a tile of 256 codewords (4 per lane): wave (g, q) evaluates leader
-group g (8 leaders) over position slice q (S positions).  All slices run the SAME code (slice 0's
-weights); slice q's partials are then multiplied by alpha^(-q S e) ("fixup").
+Main loop (tile kernel k_pt, PT_<codec>).  Per 8 positions and leader bit q the state word takes
+one 3-input XOR of two Four-Russians combinations (all 15 XORs of four position words are formed
+once per 4 positions).  A workgroup of 8 waves covers a tile of 256 codewords (4 per lane): wave
+(g, q) evaluates leader group g over the 16-position pieces of quarter q with quarter 0's networks,
+then fixes its partials up by alpha^(-16 q e) and a recursive-halving exchange sums them.
 
-Epilogue (after the partials are summed across slices): expansion (squarings) and the plane fold
-S = sum_b alpha^b V_b inside each byte (3 levels: x alpha, x alpha^2, x alpha^4 with shifts 1,2,4),
-four syndromes packed per word in the upper levels.  Output: "quads" of 8 words whose bit 8k + j
-is bit q of syndrome j of the quad for codeword k.
+Epilogue: expansion (squarings) and the plane fold S = sum_b alpha^b V_b inside each byte (3
+levels: x alpha, x alpha^2, x alpha^4 with shifts 1,2,4), four syndromes packed per word.
 
 Encode: syndromes of the data symbols (positions 0..K-1 of the full frame) go to a workspace; the
-parity kernel maps them to parity with the GF(2) matrix of  parity = V^-1 S  (V_{e,j} =
-alpha^(e (NR-1-j))), applied bit-sliced over 32 codewords per lane (q_pass, same as gen_bitslice).
+parity kernel (PS_<codec>::q_pass4) maps them to parity with the GF(2) matrix of parity = V^-1 S
+(V_{e,j} = alpha^(e (NR-1-j))), applied bit-sliced over 32 codewords per lane.
 """
 from __future__ import annotations
 
@@ -40,15 +37,25 @@ sys.path.insert(0, HERE)
 from gf8 import GF8, gf_mat_inv, lin_rows  # noqa: E402
 
 N = 255
-WAVES = 8                 # waves per workgroup (tile of 256 codewords)
-NLG = 8                   # leader slots per group (state = 8 * NLG words per wave)
-S_DEC = 64                # positions per slice: decode covers 256 (4 x 64); encode 4 x S_ENC >= K
 
-# (name, poly, fcr, prim, nroots): codecs with a plane-sliced path (leaders <= 16)
+# (name, poly, fcr, prim, nroots): codecs with a plane-sliced path.  Every RS(255,K) with
+# NROOTS <= 32 that the reference validates (rsvalidate.C:46-62), plus the conventional-basis
+# CCSDS codec RS_CCSDS_CONV(255,239) (rs:101-104; RS_CCSDS(255,223) has 27 cosets, above the
+# 16-leader tile design: it keeps the bit-sliced kernels).
 CODECS = [
     ("RS_255_223", 0x11d, 1, 1, 32),
     ("RS_255_239", 0x11d, 1, 1, 16),
     ("RS_255_251", 0x11d, 1, 1, 4),
+    ("RS_255_254", 0x11d, 1, 1, 1),
+    ("RS_255_253", 0x11d, 1, 1, 2),
+    ("RS_255_252", 0x11d, 1, 1, 3),
+    ("RS_255_248", 0x11d, 1, 1, 7),
+    ("RS_255_247", 0x11d, 1, 1, 8),
+    ("RS_255_246", 0x11d, 1, 1, 9),
+    ("RS_255_243", 0x11d, 1, 1, 12),
+    ("RS_255_238", 0x11d, 1, 1, 17),
+    ("RS_255_228", 0x11d, 1, 1, 27),
+    ("CCSDS_CONV_255_239", 0x187, 120, 11, 16),
 ]
 
 
@@ -65,8 +72,7 @@ class PsCodec:
         leaders, members = [], {}
         for i, e in enumerate(self.exps):
             for l in leaders:
-                el, k, x = self.exps[l], 0, self.exps[l]
-                found = None
+                x, found = self.exps[l], None
                 for k in range(8):
                     if x == e:
                         found = k
@@ -79,48 +85,7 @@ class PsCodec:
                 leaders.append(i)
                 members[i] = [(i, 0)]
         self.leaders, self.members = leaders, members
-        L = len(leaders)
-        assert L <= 16, "plane-sliced path supports at most 16 leaders"
-        self.R = 2
-        self.PI = WAVES // self.R
-        # encode slices: 4 x s_enc >= K data positions, a multiple of 8 (blocks of 8 positions)
-        self.s_enc = 8 * -(-(N - nr) // 32)
-        # assign leaders to (group, slot); final owner of slots {2i, 2i+1} of group g is the wave
-        # with idx(q) = 2 (q & 1) + (q >> 1) == i  (see the reduction in ezrs_ps.hip).  Pair big
-        # families with small ones so that every wave folds a similar number of syndromes.
-        order = sorted(leaders, key=lambda l: -len(members[l]))
-        pairs = []
-        lo, hi = 0, len(order) - 1
-        while lo <= hi:
-            if lo == hi:
-                pairs.append((order[lo], None))
-            else:
-                pairs.append((order[lo], order[hi]))
-            lo += 1
-            hi -= 1
-        while len(pairs) < 8:
-            pairs.append((None, None))
-        pairs.sort(key=lambda p: -sum(len(members[x]) for x in p if x is not None))
-        # spread the 8 pairs over (g, i): pair rank r -> g = r & 1, i = r >> 1
-        self.slot = {}            # leader -> (g, slot)
-        self.group = [[None] * NLG for _ in range(self.R)]
-        for r, (a, b) in enumerate(pairs):
-            g, i = r & 1, r >> 1
-            for s, l in ((2 * i, a), (2 * i + 1, b)):
-                self.group[g][s] = l
-                if l is not None:
-                    self.slot[l] = (g, s)
-        # epilogue: wave (g, q) folds the syndromes of the two leaders it owns
-        self.epi = {}
-        for g in range(self.R):
-            for i in range(4):
-                syn = []
-                for s in (2 * i, 2 * i + 1):
-                    l = self.group[g][s]
-                    if l is not None:
-                        syn += [(s - 2 * i, m, k) for m, k in members[l]]
-                self.epi[(g, i)] = syn   # (local leader 0/1, syndrome index, squarings)
-        self.nq = max((len(v) + 3) // 4 for v in self.epi.values())
+        assert len(leaders) <= 16, "plane-sliced path supports at most 16 leaders"
         # parity map: p = Vinv S  (S with the x^NR factor included)
         V = [[gf.pow_alpha(e * (nr - 1 - j)) for j in range(nr)] for e in self.exps]
         self.Vinv = gf_mat_inv(gf, V)
@@ -178,134 +143,22 @@ def mat_apply(out, dst, src, rows, ind, extra=None):
         out.extend(xor_chain(dst[q], terms, ind))
 
 
-def gen_codec(c: PsCodec):
-    gf = c.gf
+def gen_parity(c: PsCodec):
+    """PS_<codec>: the codec's constants and the parity map passes over 32-codeword bit-sliced
+    syndromes, q_pass4<P> = parity symbols 4P .. 4P+3 (k_ps_parity8, wave P)."""
     st = f"PS_{c.name}"
     out = [f"struct {st} {{",
            f"    static constexpr unsigned POLY = {c.poly:#x}, FCR = {c.fcr}, PRIM = {c.prim}, NR = {c.nr};",
-           f"    static constexpr int R = {c.R}, PI = {c.PI}, NLG = {NLG}, NQ = {c.nq};",
-           f"    static constexpr int S_DEC = {S_DEC}, S_ENC = {c.s_enc};",
-           "    // main loop: positions 8B..8B+7 of slice 0 (words X[0..7]) into group G's state",
-           "    template <int G, int B> static __device__ void block(uint32_t (&V)[NLG][8], const uint32_t (&X)[8]);",
-           "    // slice-q partials of group G times alpha^(-q S e) (S = S_DEC or S_ENC)",
-           "    template <int G, int S> static __device__ void fixup(uint32_t (&V)[NLG][8], int q);",
-           "    // wave (G, I) epilogue: the totals of its two leaders -> NQ quads of syndromes",
-           "    template <int G, int I> static __device__ void epilogue(const uint32_t (&T)[2][8], uint32_t (&Q)[NQ][8]);",
-           "    // syndrome index of quad slot (wave (G, I), quad, j), -1 = none",
-           f"    static constexpr int SYN[{c.R}][4][{c.nq}][4] = " + "{" + ", ".join(
-               "{" + ", ".join("{" + ", ".join(
-                   "{" + ", ".join(str(c.epi[(g, i)][4 * qd + j][1]) if 4 * qd + j < len(c.epi[(g, i)]) else "-1"
-                                   for j in range(4)) + "}" for qd in range(c.nq)) + "}"
-                   for i in range(4)) + "}" for g in range(c.R)) + "};",
-           "    template <int P> static __device__ void q_pass(uint32_t (&O)[8][8], const uint32_t *in, int ld);",
            "    template <int P> static __device__ void q_pass4(uint32_t (&O)[4][8], const uint32_t *in, int ld);",
-           f"    static constexpr int NPASS = {(c.nr + 7) // 8}, NPASS4 = {(c.nr + 3) // 4};",
+           f"    static constexpr int NPASS4 = {(c.nr + 3) // 4};",
            "};"]
     I = "    "
-    # ---- main-loop blocks
-    for g in range(c.R):
-        for B in range(S_DEC // 8):
-            out.append(f"template <> __device__ __forceinline__ void {st}::block<{g}, {B}>("
-                       "uint32_t (&V)[NLG][8], const uint32_t (&X)[8]) {")
-            emit_combos(out, "l", [f"X[{t}]" for t in range(4)], I)
-            emit_combos(out, "h", [f"X[{t}]" for t in range(4, 8)], I)
-            for s in range(NLG):
-                l = c.group[g][s]
-                if l is None:
-                    continue
-                for q in range(8):
-                    m1 = sum(((c.w(l, 8 * B + t) >> q) & 1) << t for t in range(4))
-                    m2 = sum(((c.w(l, 8 * B + 4 + t) >> q) & 1) << t for t in range(4))
-                    terms = ([f"l{m1}"] if m1 else []) + ([f"h{m2}"] if m2 else [])
-                    if len(terms) == 2:
-                        out.append(f"{I}V[{s}][{q}] = xor3(V[{s}][{q}], {terms[0]}, {terms[1]});")
-                    elif terms:
-                        out.append(f"{I}V[{s}][{q}] ^= {terms[0]};")
-            out.append("}")
-    # ---- fixups
-    for g in range(c.R):
-        for S in sorted({S_DEC, c.s_enc}):
-            out.append(f"template <> __device__ __forceinline__ void {st}::fixup<{g}, {S}>("
-                       "uint32_t (&V)[NLG][8], int q) {")
-            out.append(f"{I}uint32_t t[8];")
-            out.append(f"{I}switch (q) {{")
-            for qq in range(1, c.PI):
-                out.append(f"{I}case {qq}:")
-                for s in range(NLG):
-                    l = c.group[g][s]
-                    if l is None:
-                        continue
-                    cst = gf.pow_alpha((-qq * S * c.exps[l]) % N)
-                    rows = lin_rows(lambda x, cst=cst: gf.mul(cst, x))
-                    out.append(f"{I}    for (int b = 0; b < 8; ++b) t[b] = V[{s}][b];")
-                    mat_apply(out, [f"V[{s}][{q}]" for q in range(8)], [f"t[{b}]" for b in range(8)], rows, I + "    ")
-                out.append(f"{I}    break;")
-            out.append(f"{I}default: break;")
-            out.append(f"{I}}}")
-            out.append("}")
-    # ---- epilogues
-    sq_rows = {}
-
-    def sqk_rows(k):
-        if k not in sq_rows:
-            sq_rows[k] = lin_rows(lambda x, k=k: gf.pow(x, 1 << k) if x else 0)
-        return sq_rows[k]
-
-    a1 = lin_rows(lambda x: gf.mul(2, x))
-    a2 = lin_rows(lambda x: gf.mul(4, x))
-    a4 = lin_rows(lambda x: gf.mul(16, x))
-
-    def fold_level(out, dst, src, rows, sh, ind):
-        # dst[q] = src[q] ^ (alpha-matrix applied to (src >> sh))[q]
-        out.append(f"{ind}{{")
-        out.append(f"{ind}    uint32_t y[8];")
-        out.append(f"{ind}    for (int b = 0; b < 8; ++b) y[b] = {src}[b] >> {sh};")
-        mat_apply(out, [f"{dst}[{q}]" for q in range(8)], [f"y[{b}]" for b in range(8)], rows, ind + "    ",
-                  extra=[f"{src}[{q}]" for q in range(8)])
-        out.append(f"{ind}}}")
-
-    for g in range(c.R):
-        for i in range(4):
-            syn = c.epi[(g, i)]
-            out.append(f"template <> __device__ __forceinline__ void {st}::epilogue<{g}, {i}>("
-                       "const uint32_t (&T)[2][8], uint32_t (&Q)[NQ][8]) {")
-            for qd in range(c.nq):
-                part = syn[4 * qd:4 * qd + 4]
-                out.append(f"{I}{{ // quad {qd}: syndromes {[m for _, m, _ in part]}")
-                # level 1 per syndrome
-                for j in range(4):
-                    out.append(f"{I}    uint32_t F{j}[8];")
-                    if j < len(part):
-                        ll, m, k = part[j]
-                        if k == 0:
-                            out.append(f"{I}    const uint32_t *W{j} = T[{ll}];")
-                        else:
-                            out.append(f"{I}    uint32_t W{j}[8];")
-                            mat_apply(out, [f"W{j}[{q}]" for q in range(8)], [f"T[{ll}][{b}]" for b in range(8)],
-                                      sqk_rows(k), I + "    ")
-                        fold_level(out, f"F{j}", f"W{j}", a1, 1, I + "    ")
-                    else:
-                        out.append(f"{I}    for (int b = 0; b < 8; ++b) F{j}[b] = 0u;")
-                # pack pairs, level 2
-                for pj in range(2):
-                    out.append(f"{I}    uint32_t P{pj}[8], G{pj}[8];")
-                    out.append(f"{I}    for (int b = 0; b < 8; ++b) P{pj}[b] = bfi(0x55555555u, "
-                               f"F{2 * pj}[b], F{2 * pj + 1}[b] << 1);")
-                    fold_level(out, f"G{pj}", f"P{pj}", a2, 2, I + "    ")
-                out.append(f"{I}    uint32_t H[8];")
-                out.append(f"{I}    for (int b = 0; b < 8; ++b) H[b] = bfi(0x33333333u, "
-                           f"G0[b], G1[b] << 2);")
-                fold_level(out, f"Q[{qd}]", "H", a4, 4, I + "    ")
-                out.append(f"{I}}}")
-            out.append("}")
-    # ---- parity map passes over 32-codeword bit-sliced syndromes: q_pass (8 parity symbols per
-    # pass) and q_pass4 (4 per pass, for the 8-wave parity kernel)
     Q = c.q_rows()
     nr = c.nr
-    for PW, fname in ((8, "q_pass"), (4, "q_pass4")):
-      for P in range((nr + PW - 1) // PW):
+    PW = 4
+    for P in range((nr + PW - 1) // PW):
         j0, nj = PW * P, min(PW, nr - PW * P)
-        out.append(f"template <> __device__ __forceinline__ void {st}::{fname}<{P}>("
+        out.append(f"template <> __device__ __forceinline__ void {st}::q_pass4<{P}>("
                    f"uint32_t (&O)[{PW}][8], const uint32_t *in, int ld) {{")
         first = [[True] * 8 for _ in range(nj)]
         out.append(f"{I}uint32_t N[8];")
@@ -340,287 +193,6 @@ def gen_codec(c: PsCodec):
             out.append(f"{I}}}")
         out.append("}")
     return "\n".join(out)
-
-
-def gen_pw(c: PsCodec):
-    """Per-wave variant: one wave owns 256 codewords and ALL leaders (state NL x 8 words), walks every
-    position itself (no slices, no fixups, no cross-wave reduction) and folds all NR syndromes."""
-    gf = c.gf
-    st = f"PW_{c.name}"
-    L = len(c.leaders)
-    # epilogue order: leaders by family size (largest first), members by squaring count, so a
-    # leader's state dies as soon as its family is folded
-    seq = []
-    for li, l in sorted(enumerate(c.leaders), key=lambda x: -len(c.members[x[1]])):
-        for m, k in sorted(c.members[l], key=lambda x: x[1]):
-            seq.append((li, m, k))
-    nq = (len(seq) + 3) // 4
-    syn = [[seq[4 * qd + j][1] if 4 * qd + j < len(seq) else -1 for j in range(4)] for qd in range(nq)]
-    out = [f"struct {st} {{",
-           f"    static constexpr unsigned POLY = {c.poly:#x}, FCR = {c.fcr}, PRIM = {c.prim}, NR = {c.nr};",
-           f"    static constexpr int NL = {L}, NQ = {nq};",
-           "    // positions 8B..8B+7 of the full frame (words X[0..7]) into the state",
-           "    template <int B> static __device__ void block(uint32_t (&V)[NL][8], const uint32_t (&X)[8]);",
-           "    // all syndromes, four per quad; emit(integral_constant<qd>, Q[8]) per quad",
-           "    template <class F> static __device__ void epilogue(const uint32_t (&V)[NL][8], F &&emit);",
-           f"    static constexpr int SYN[{nq}][4] = " + "{" + ", ".join(
-               "{" + ", ".join(str(x) for x in row) + "}" for row in syn) + "};",
-           "};"]
-    I = "    "
-    for B in range(32):
-        out.append(f"template <> __device__ __forceinline__ void {st}::block<{B}>("
-                   "uint32_t (&V)[NL][8], const uint32_t (&X)[8]) {")
-        emit_combos(out, "l", [f"X[{t}]" for t in range(4)], I)
-        emit_combos(out, "h", [f"X[{t}]" for t in range(4, 8)], I)
-        for s, l in enumerate(c.leaders):
-            for q in range(8):
-                m1 = sum(((c.w(l, 8 * B + t) >> q) & 1) << t for t in range(4))
-                m2 = sum(((c.w(l, 8 * B + 4 + t) >> q) & 1) << t for t in range(4))
-                terms = ([f"l{m1}"] if m1 else []) + ([f"h{m2}"] if m2 else [])
-                if len(terms) == 2:
-                    out.append(f"{I}V[{s}][{q}] = xor3(V[{s}][{q}], {terms[0]}, {terms[1]});")
-                elif terms:
-                    out.append(f"{I}V[{s}][{q}] ^= {terms[0]};")
-        out.append("}")
-
-    sq_cache = {}
-
-    def sqk(k):
-        if k not in sq_cache:
-            sq_cache[k] = lin_rows(lambda x, k=k: gf.pow(x, 1 << k) if x else 0)
-        return sq_cache[k]
-
-    def cost(rows):
-        return sum(max(0, bin(r).count("1") - 1) for r in rows)
-
-    a1 = lin_rows(lambda x: gf.mul(2, x))
-    a2 = lin_rows(lambda x: gf.mul(4, x))
-    a4 = lin_rows(lambda x: gf.mul(16, x))
-
-    def fold_level(dst, src, rows, sh, ind):
-        out.append(f"{ind}{{")
-        out.append(f"{ind}    uint32_t y[8];")
-        out.append(f"{ind}    for (int b = 0; b < 8; ++b) y[b] = {src}[b] >> {sh};")
-        mat_apply(out, [f"{dst}[{q}]" for q in range(8)], [f"y[{b}]" for b in range(8)], rows, ind + "    ",
-                  extra=[f"{src}[{q}]" for q in range(8)])
-        out.append(f"{ind}}}")
-
-    out.append(f"template <class F> __device__ __forceinline__ void {st}::epilogue("
-               "const uint32_t (&V)[NL][8], F &&emit) {")
-    # expansion: member (li, k) from V[li] (sq^k) or from the previous member (sq^(k - k')),
-    # computed right before its quad so that few expanded values are live at once
-    prev = {}
-
-    def expand(li, m, k, ind):
-        if k == 0:
-            prev[li] = (f"V[{li}]", 0)
-            return f"V[{li}]"
-        src, kp = prev[li]
-        direct = cost(sqk(k))
-        chained = cost(sqk(k - kp)) if kp else direct
-        out.append(f"{ind}uint32_t W{m}[8];")
-        if kp and chained < direct:
-            mat_apply(out, [f"W{m}[{q}]" for q in range(8)], [f"{src}[{b}]" for b in range(8)], sqk(k - kp), ind)
-        else:
-            mat_apply(out, [f"W{m}[{q}]" for q in range(8)], [f"V[{li}][{b}]" for b in range(8)], sqk(k), ind)
-        prev[li] = (f"W{m}", k)
-        return f"W{m}"
-
-    for qd in range(nq):
-        part = seq[4 * qd:4 * qd + 4]
-        srcs = [expand(li, m, k, I) for li, m, k in part]
-        out.append(f"{I}{{ // quad {qd}: syndromes {[m for _, m, _ in part]}")
-        for j in range(4):
-            out.append(f"{I}    uint32_t F{j}[8];")
-            if j < len(part):
-                fold_level(f"F{j}", srcs[j], a1, 1, I + "    ")
-            else:
-                out.append(f"{I}    for (int b = 0; b < 8; ++b) F{j}[b] = 0u;")
-        for pj in range(2):
-            out.append(f"{I}    uint32_t P{pj}[8], G{pj}[8];")
-            out.append(f"{I}    for (int b = 0; b < 8; ++b) P{pj}[b] = bfi(0x55555555u, "
-                       f"F{2 * pj}[b], F{2 * pj + 1}[b] << 1);")
-            fold_level(f"G{pj}", f"P{pj}", a2, 2, I + "    ")
-        out.append(f"{I}    uint32_t H[8], Q[8];")
-        out.append(f"{I}    for (int b = 0; b < 8; ++b) H[b] = bfi(0x33333333u, G0[b], G1[b] << 2);")
-        fold_level("Q", "H", a4, 4, I + "    ")
-        out.append(f"{I}    emit(std::integral_constant<int, {qd}>{{}}, Q);")
-        out.append(f"{I}}}")
-    out.append("}")
-    return "\n".join(out)
-
-
-def py_split(c: PsCodec):
-    """Split the leaders between the two waves of the pair kernel: each wave owns NL/2 leaders;
-    minimise the larger wave's quad count, then the syndrome imbalance."""
-    from itertools import combinations
-    L = len(c.leaders)
-    sizes = [len(c.members[l]) for l in c.leaders]
-    half = L // 2
-    best = None
-    for comb in combinations(range(L), half):
-        n0 = sum(sizes[i] for i in comb)
-        n1 = sum(sizes) - n0
-        key = (max((n0 + 3) // 4, (n1 + 3) // 4), (n0 + 3) // 4 + (n1 + 3) // 4, abs(n0 - n1))
-        if best is None or key < best[0]:
-            best = (key, comb)
-    own0 = list(best[1])
-    own1 = [i for i in range(L) if i not in own0]
-    return [own0, own1]
-
-
-def gen_py(c: PsCodec):
-    """Pair variant: two waves share 128-position windows of a 256-codeword tile; wave q evaluates
-    ALL leaders over positions [64 q, 64 q + 64) of each window (the PW blocks of those positions:
-    no fixups), then the waves swap the partials of the leaders the other one owns (NL/2 each) and
-    fold their own leaders' syndromes."""
-    gf = c.gf
-    st = f"PY_{c.name}"
-    L = len(c.leaders)
-    assert L % 2 == 0, "pair kernel needs an even leader count"
-    own = py_split(c)
-    NLW = L // 2
-    seqs = []
-    for q in range(2):
-        seq = []
-        for li in sorted(own[q], key=lambda i: -len(c.members[c.leaders[i]])):
-            loc = own[q].index(li)
-            for m, k in sorted(c.members[c.leaders[li]], key=lambda x: x[1]):
-                seq.append((loc, m, k))
-        seqs.append(seq)
-    nq = max((len(s) + 3) // 4 for s in seqs)
-    out = [f"struct {st} : PW_{c.name} {{",
-           f"    static constexpr int NLW = {NLW}, NQW = {nq};",
-           f"    static constexpr int OWN[2][{NLW}] = " + "{" + ", ".join(fmt_list(o) for o in own) + "};",
-           "    // wave Q's syndromes from the totals of its own leaders (T[i] <-> leader OWN[Q][i])",
-           "    template <int Q, class F> static __device__ void epilogue(const uint32_t (&T)[NLW][8], F &&emit);",
-           f"    static constexpr int SYN[2][{nq}][4] = " + "{" + ", ".join(
-               "{" + ", ".join("{" + ", ".join(str(seqs[q][4 * qd + j][1]) if 4 * qd + j < len(seqs[q]) else "-1"
-                                               for j in range(4)) + "}" for qd in range(nq)) + "}"
-               for q in range(2)) + "};",
-           "};"]
-    I = "    "
-    sq_cache = {}
-
-    def sqk(k):
-        if k not in sq_cache:
-            sq_cache[k] = lin_rows(lambda x, k=k: gf.pow(x, 1 << k) if x else 0)
-        return sq_cache[k]
-
-    def cost(rows):
-        return sum(max(0, bin(r).count("1") - 1) for r in rows)
-
-    a1 = lin_rows(lambda x: gf.mul(2, x))
-    a2 = lin_rows(lambda x: gf.mul(4, x))
-    a4 = lin_rows(lambda x: gf.mul(16, x))
-
-    def fold_level(dst, src, rows, sh, ind):
-        out.append(f"{ind}{{")
-        out.append(f"{ind}    uint32_t y[8];")
-        out.append(f"{ind}    for (int b = 0; b < 8; ++b) y[b] = {src}[b] >> {sh};")
-        mat_apply(out, [f"{dst}[{q}]" for q in range(8)], [f"y[{b}]" for b in range(8)], rows, ind + "    ",
-                  extra=[f"{src}[{q}]" for q in range(8)])
-        out.append(f"{ind}}}")
-
-    for q in range(2):
-        seq = seqs[q]
-        out.append(f"template <class F> __device__ __forceinline__ void {st}_epi{q}("
-                   f"const uint32_t (&T)[{st}::NLW][8], F &&emit) {{")
-        prev = {}
-
-        def expand(li, m, k, ind):
-            if k == 0:
-                prev[li] = (f"T[{li}]", 0)
-                return f"T[{li}]"
-            src, kp = prev[li]
-            direct = cost(sqk(k))
-            chained = cost(sqk(k - kp)) if kp else direct
-            out.append(f"{ind}uint32_t W{m}[8];")
-            if kp and chained < direct:
-                mat_apply(out, [f"W{m}[{b}]" for b in range(8)], [f"{src}[{b}]" for b in range(8)], sqk(k - kp), ind)
-            else:
-                mat_apply(out, [f"W{m}[{b}]" for b in range(8)], [f"T[{li}][{b}]" for b in range(8)], sqk(k), ind)
-            prev[li] = (f"W{m}", k)
-            return f"W{m}"
-
-        for qd in range((len(seq) + 3) // 4):
-            part = seq[4 * qd:4 * qd + 4]
-            srcs = [expand(li, m, k, I) for li, m, k in part]
-            out.append(f"{I}{{ // quad {qd}: syndromes {[m for _, m, _ in part]}")
-            for j in range(4):
-                out.append(f"{I}    uint32_t F{j}[8];")
-                if j < len(part):
-                    fold_level(f"F{j}", srcs[j], a1, 1, I + "    ")
-                else:
-                    out.append(f"{I}    for (int b = 0; b < 8; ++b) F{j}[b] = 0u;")
-            for pj in range(2):
-                out.append(f"{I}    uint32_t P{pj}[8], G{pj}[8];")
-                out.append(f"{I}    for (int b = 0; b < 8; ++b) P{pj}[b] = bfi(0x55555555u, "
-                           f"F{2 * pj}[b], F{2 * pj + 1}[b] << 1);")
-                fold_level(f"G{pj}", f"P{pj}", a2, 2, I + "    ")
-            out.append(f"{I}    uint32_t H[8], Q[8];")
-            out.append(f"{I}    for (int b = 0; b < 8; ++b) H[b] = bfi(0x33333333u, G0[b], G1[b] << 2);")
-            fold_level("Q", "H", a4, 4, I + "    ")
-            out.append(f"{I}    emit(std::integral_constant<int, {qd}>{{}}, Q);")
-            out.append(f"{I}}}")
-        out.append("}")
-    out.append(f"template <int Q, class F> __device__ __forceinline__ void {st}::epilogue("
-               "const uint32_t (&T)[NLW][8], F &&emit) {")
-    out.append(f"{I}if constexpr (Q == 0) {st}_epi0(T, emit); else {st}_epi1(T, emit);")
-    out.append("}")
-    return "\n".join(out)
-
-
-def pg_split(c: PsCodec, nw: int, even_levels: int = 1):
-    """Leaders -> nw owner waves by recursive halving (the exchange rounds halve the set each
-    time): at each level the two halves hold equal leader counts (so every round sends at most
-    half), minimising the largest quad count over the final groups, then their sum."""
-    from functools import lru_cache
-    from itertools import combinations
-    size = [len(c.members[l]) for l in c.leaders]
-    L = len(size)
-
-    def quads(g):
-        return -(-sum(size[j] for j in g) // 4)
-
-    @lru_cache(maxsize=None)
-    def best(items, n):
-        """Best split of the frozenset items into n groups: (score, groups)."""
-        items = tuple(sorted(items))
-        if n == 1:
-            q = quads(items)
-            return (q, q), [list(items)]
-        res = None
-        # the top level (exchange round 0, the big one) splits the leaders evenly; the last level
-        # may split them any way (its round sends at most the half anyway)
-        level = (nw // n).bit_length() - 1                  # 0 at the top
-        sizes = [len(items) // 2] if level < even_levels else range(0, len(items) + 1)
-        for k in sizes:
-            combs = combinations(items, k)
-            if level < even_levels and len(items) % 2 == 0:
-                combs = ((items[0],) + cmb for cmb in combinations(items[1:], k - 1))   # symmetry
-            for A in combs:
-                B = tuple(i for i in items if i not in A)
-                sa, ga = best(frozenset(A), n // 2)
-                sb, gb = best(frozenset(B), n // 2)
-                sc = (max(sa[0], sb[0]), sa[1] + sb[1])
-                if res is None or sc < res[0]:
-                    res = (sc, ga + gb)
-        return res
-    # group order: wave q's leaders; the recursion's nesting matches the exchange (bit r of q
-    # selects the half at level r from the bottom), so interleave: groups [g0, g1, g2, g3] of the
-    # nested split ((g0, g1), (g2, g3)) go to waves 0, 2, 1, 3
-    _, groups = best(frozenset(range(L)), nw)
-    order = []
-    for q in range(nw):
-        # wave q: its bit 0 selects the top-level half, bit 1 the half within it, ...
-        idx, span, lo = 0, nw, 0
-        for r in range(nw.bit_length() - 1):
-            span //= 2
-            if q >> r & 1:
-                lo += span
-        order.append(groups[lo])
-    return [sorted(g) for g in order]
 
 
 def emit_fold_epilogue(out, gf, fname, T, nlw_expr, seq):
@@ -691,169 +263,6 @@ def emit_fold_epilogue(out, gf, fname, T, nlw_expr, seq):
     out.append("}")
 
 
-def gen_pg(c: PsCodec, nw: int):
-    """Group variant: nw waves share a whole 256-codeword tile in LDS (two 128-position halves in
-    the swizzled gather layout); wave q evaluates ALL leaders over the 16-position pieces
-    g = q, q + nw, ... of the tile with the PW blocks of those positions (no fixups); then
-    log2(nw) rounds of pairwise exchange (recursive halving by owner bits) leave every wave the
-    totals of the leaders it owns, whose syndromes it folds."""
-    gf = c.gf
-    st = f"PG{nw}_{c.name}"
-    L = len(c.leaders)
-    own = pg_split(c, nw)
-    nlw = max(len(o) for o in own)
-    owner = {}
-    for q, o in enumerate(own):
-        for s_ in o:
-            owner[s_] = q
-    rounds = nw.bit_length() - 1
-    # per round r and wave q: leaders sent / kept (kept order == partner's sent order)
-    send = [[None] * rounds for _ in range(nw)]
-    keep = [[None] * rounds for _ in range(nw)]
-    for q in range(nw):
-        K = list(range(L))
-        for r in range(rounds):
-            bit = 1 << r
-            send[q][r] = [s_ for s_ in K if (owner[s_] & bit) != (q & bit)]
-            keep[q][r] = [s_ for s_ in K if (owner[s_] & bit) == (q & bit)]
-            K = keep[q][r]
-    nsend = [max(len(send[q][r]) for q in range(nw)) for r in range(rounds)]
-    seqs = []
-    for q in range(nw):
-        seq = []
-        for li in sorted(own[q], key=lambda i: -len(c.members[c.leaders[i]])):
-            loc = own[q].index(li)
-            for m, k in sorted(c.members[c.leaders[li]], key=lambda x: x[1]):
-                seq.append((loc, m, k))
-        seqs.append(seq)
-    nq = max(1, max((len(s_) + 3) // 4 for s_ in seqs))
-
-    def pad(xs, n):
-        return list(xs) + [-1] * (n - len(xs))
-    out = [f"struct {st} : PW_{c.name} {{",
-           f"    static constexpr int NW = {nw}, NLW = {nlw}, NQW = {nq}, ROUNDS = {rounds};",
-           f"    static constexpr int OWN[{nw}][{nlw}] = " + "{" + ", ".join(fmt_list(pad(o, nlw)) for o in own) + "};",
-           f"    static constexpr int NSEND[{max(rounds, 1)}] = {fmt_list(nsend or [0])};",
-           f"    static constexpr int SEND[{nw}][{max(rounds, 1)}][{max(nsend or [1])}] = " + "{" + ", ".join(
-               "{" + ", ".join(fmt_list(pad(send[q][r], max(nsend))) for r in range(rounds)) + "}" for q in range(nw)) + "};",
-           f"    static constexpr int KEEP[{nw}][{max(rounds, 1)}][{max(nsend or [1])}] = " + "{" + ", ".join(
-               "{" + ", ".join(fmt_list(pad(send[q ^ (1 << r)][r], max(nsend))) for r in range(rounds)) + "}"
-               for q in range(nw)) + "};",
-           "    // wave Q's syndromes from the totals of its own leaders (T[i] <-> leader OWN[Q][i])",
-           "    template <int Q, class F> static __device__ void epilogue(const uint32_t (&T)[NLW][8], F &&emit);",
-           f"    static constexpr int SYN[{nw}][{nq}][4] = " + "{" + ", ".join(
-               "{" + ", ".join("{" + ", ".join(str(seqs[q][4 * qd + j][1]) if 4 * qd + j < len(seqs[q]) else "-1"
-                                               for j in range(4)) + "}" for qd in range(nq)) + "}"
-               for q in range(nw)) + "};",
-           "};"]
-    for q in range(nw):
-        emit_fold_epilogue(out, gf, f"{st}_epi{q}", "T", f"{st}::NLW", seqs[q])
-    out.append(f"template <int Q, class F> __device__ __forceinline__ void {st}::epilogue("
-               "const uint32_t (&T)[NLW][8], F &&emit) {")
-    out.append("    " + " else ".join(f"if constexpr (Q == {q}) {st}_epi{q}(T, emit);" for q in range(nw)))
-    out.append("}")
-    return "\n".join(out)
-
-
-def gen_pg8(c: PsCodec):
-    """8-wave group variant: one workgroup per CU, whole tiles double-buffered in LDS; wave
-    w = 4 g + q evaluates leader group g (half the leaders) over the pieces q, q + 4, q + 8, q + 12
-    of the tile; the 4 waves of a group then exchange in two rounds (recursive halving by owner
-    bits) so that each owns the totals of its leaders."""
-    gf = c.gf
-    st = f"PG8_{c.name}"
-    L = len(c.leaders)
-    assert L % 2 == 0
-    own = pg_split(c, 8, even_levels=2)                    # waves 0..7; bit 0 of the wave id = top split
-    # top-level split (bit 0 of the wave id) = the leader group; re-index waves as 4 g + q
-    groups = [sorted(own[0] + own[2] + own[4] + own[6]), sorted(own[1] + own[3] + own[5] + own[7])]
-    W = {}                                                 # (g, q) -> owned global leaders
-    for w8 in range(8):
-        g, qq = w8 & 1, w8 >> 1                            # qq bits = the lower split levels
-        W[(g, qq)] = own[w8]
-    nlg = L // 2
-    loc = [{l: i for i, l in enumerate(groups[g])} for g in range(2)]
-    rounds = 2
-    send, keep = {}, {}
-    for g in range(2):
-        ownerq = {}
-        for q in range(4):
-            for l in W[(g, q)]:
-                ownerq[l] = q
-        for q in range(4):
-            K = list(groups[g])
-            for r in range(rounds):
-                bit = 1 << r
-                send[(g, q, r)] = [loc[g][l] for l in K if (ownerq[l] & bit) != (q & bit)]
-                keep[(g, q, r)] = [l for l in K if (ownerq[l] & bit) == (q & bit)]
-                K = keep[(g, q, r)]
-    nsend = [max(len(send[(g, q, r)]) for g in range(2) for q in range(4)) for r in range(rounds)]
-    nlw = max(len(W[k]) for k in W)
-    seqs = {}
-    for g in range(2):
-        for q in range(4):
-            seq = []
-            ow = W[(g, q)]
-            for li in sorted(ow, key=lambda i: -len(c.members[c.leaders[i]])):
-                for m, k in sorted(c.members[c.leaders[li]], key=lambda x: x[1]):
-                    seq.append((ow.index(li), m, k))
-            seqs[(g, q)] = seq
-    nq = max(1, max((len(v) + 3) // 4 for v in seqs.values()))
-
-    def pad(xs, n):
-        return list(xs) + [-1] * (n - len(xs))
-    ms = max(nsend)
-    out = [f"struct {st} {{",
-           f"    static constexpr unsigned POLY = {c.poly:#x}, FCR = {c.fcr}, PRIM = {c.prim}, NR = {c.nr};",
-           f"    static constexpr int NLG = {nlg}, NLW = {nlw}, NQW = {nq}, ROUNDS = {rounds};",
-           "    // positions 8B..8B+7 (words X[0..7]) into the state of leader group G",
-           "    template <int G, int B> static __device__ void block(uint32_t (&V)[NLG][8], const uint32_t (&X)[8]);",
-           f"    static constexpr int NSEND[{rounds}] = {fmt_list(nsend)};",
-           "    // [g][q][round][i]: local leader slots sent to / received from the partner q ^ (1 << round)",
-           f"    static constexpr int SEND[2][4][{rounds}][{ms}] = " + "{" + ", ".join(
-               "{" + ", ".join("{" + ", ".join(fmt_list(pad(send[(g, q, r)], ms)) for r in range(rounds)) + "}"
-                               for q in range(4)) + "}" for g in range(2)) + "};",
-           f"    static constexpr int KEEP[2][4][{rounds}][{ms}] = " + "{" + ", ".join(
-               "{" + ", ".join("{" + ", ".join(fmt_list(pad(send[(g, q ^ (1 << r), r)], ms)) for r in range(rounds)) + "}"
-                               for q in range(4)) + "}" for g in range(2)) + "};",
-           f"    static constexpr int OWN[2][4][{nlw}] = " + "{" + ", ".join(
-               "{" + ", ".join(fmt_list(pad([loc[g][l] for l in W[(g, q)]], nlw)) for q in range(4)) + "}"
-               for g in range(2)) + "};",
-           "    template <int G, int Q, class F> static __device__ void epilogue(const uint32_t (&T)[NLW][8], F &&emit);",
-           f"    static constexpr int SYN[2][4][{nq}][4] = " + "{" + ", ".join(
-               "{" + ", ".join("{" + ", ".join("{" + ", ".join(
-                   str(seqs[(g, q)][4 * qd + j][1]) if 4 * qd + j < len(seqs[(g, q)]) else "-1" for j in range(4)) + "}"
-                   for qd in range(nq)) + "}" for q in range(4)) + "}" for g in range(2)) + "};",
-           "};"]
-    I = "    "
-    for g in range(2):
-        for B in range(32):
-            out.append(f"template <> __device__ __forceinline__ void {st}::block<{g}, {B}>("
-                       "uint32_t (&V)[NLG][8], const uint32_t (&X)[8]) {")
-            emit_combos(out, "l", [f"X[{t}]" for t in range(4)], I)
-            emit_combos(out, "h", [f"X[{t}]" for t in range(4, 8)], I)
-            for s_, li in enumerate(groups[g]):
-                l = c.leaders[li]
-                for q in range(8):
-                    m1 = sum(((c.w(l, 8 * B + t) >> q) & 1) << t for t in range(4))
-                    m2 = sum(((c.w(l, 8 * B + 4 + t) >> q) & 1) << t for t in range(4))
-                    terms = ([f"l{m1}"] if m1 else []) + ([f"h{m2}"] if m2 else [])
-                    if len(terms) == 2:
-                        out.append(f"{I}V[{s_}][{q}] = xor3(V[{s_}][{q}], {terms[0]}, {terms[1]});")
-                    elif terms:
-                        out.append(f"{I}V[{s_}][{q}] ^= {terms[0]};")
-            out.append("}")
-    for g in range(2):
-        for q in range(4):
-            emit_fold_epilogue(out, gf, f"{st}_epi{g}{q}", "T", f"{st}::NLW", seqs[(g, q)])
-    out.append(f"template <int G, int Q, class F> __device__ __forceinline__ void {st}::epilogue("
-               "const uint32_t (&T)[NLW][8], F &&emit) {")
-    out.append("    " + " else ".join(f"if constexpr (G == {g} && Q == {q}) {st}_epi{g}{q}(T, emit);"
-                                     for g in range(2) for q in range(4)))
-    out.append("}")
-    return "\n".join(out)
-
-
 def emit_weight_block(out, fname_sig, weights, B, I="    "):
     """One main-loop block: positions 8B..8B+7 (X[0..7]) into state V[s][q] for the GF(2^8)
     weight functions weights[s](p) (V[s] accumulates sum_p bit_b(x_p) weights[s](p))."""
@@ -870,123 +279,6 @@ def emit_weight_block(out, fname_sig, weights, B, I="    "):
             elif terms:
                 out.append(f"{I}V[{s_}][{q}] ^= {terms[0]};")
     out.append("}")
-
-
-def pz_split(c: PsCodec, nw: int = 4):
-    """Leaders -> nw waves for the position-complete kernel, balancing the per-wave VALU: the main
-    loop costs ~8 per leader per block on top of a fixed ~62 (loads, transposes, combinations),
-    the fold ~300 per quad of syndromes.  Greedy, then moves/swaps while the maximum drops."""
-    size = [len(c.members[l]) for l in c.leaders]
-    L = len(size)
-
-    def cost(g):
-        return 32 * (62 + 8 * len(g)) + 300 * (-(-sum(size[j] for j in g) // 4))
-
-    def score(gs):
-        cs = sorted((cost(g) for g in gs), reverse=True)
-        return tuple(cs)
-    groups = [[] for _ in range(nw)]
-    for i in sorted(range(L), key=lambda i: -size[i]):
-        min(groups, key=lambda g: cost(g + [i])).append(i)
-    improved = True
-    while improved:
-        improved = False
-        for a in range(nw):
-            for b in range(nw):
-                if a == b:
-                    continue
-                for ia in range(len(groups[a])):
-                    cands = [("m", None)] + [("s", ib) for ib in range(len(groups[b]))]
-                    for kind, ib in cands:
-                        gs = [list(g) for g in groups]
-                        if kind == "m":
-                            gs[b].append(gs[a].pop(ia))
-                        else:
-                            gs[a][ia], gs[b][ib] = gs[b][ib], gs[a][ia]
-                        if score(gs) < score(groups):
-                            groups, improved = gs, True
-                            break
-                    if improved:
-                        break
-                if improved:
-                    break
-            if improved:
-                break
-    return [sorted(g) for g in groups]
-
-
-def gen_pz(c: PsCodec):
-    """Position-complete variant (no exchange): 4 waves share a whole tile in LDS and each walks
-    ALL positions for its own outputs.
-      decode: wave q evaluates its own leaders (4 groups balanced by quad count) and folds their
-              syndromes;
-      encode: wave q computes parity symbols 8q..8q+7 DIRECTLY from the data positions with the
-              systematic generator weights G[p][j] = sum_i Vinv[j][i] alpha^(e_i (N-1-p)) (parity
-              is GF(2^8)-linear in the data), then folds them -- no syndromes, no parity pass."""
-    gf = c.gf
-    st = f"PZ_{c.name}"
-    own = pz_split(c, 4)
-    nlw = max(len(o) for o in own)
-    nr = c.nr
-    npar = -(-nr // 4)                                    # parity symbols per wave (<= 8)
-    seqs = []
-    for q in range(4):
-        seq = []
-        for li in sorted(own[q], key=lambda i: -len(c.members[c.leaders[i]])):
-            for m, k in sorted(c.members[c.leaders[li]], key=lambda x: x[1]):
-                seq.append((own[q].index(li), m, k))
-        seqs.append(seq)
-    nqd = max(1, max((len(s_) + 3) // 4 for s_ in seqs))
-    nqe = -(-npar // 4)
-    K = N - nr
-
-    def G(p, j):
-        acc = 0
-        for i in range(nr):
-            acc ^= gf.mul(c.Vinv[j][i], gf.pow_alpha(c.exps[i] * (N - 1 - p)))
-        return acc
-    Gt = [[G(p, j) for j in range(nr)] for p in range(K)]
-
-    def pad(xs, n):
-        return list(xs) + [-1] * (n - len(xs))
-    out = [f"struct {st} {{",
-           f"    static constexpr unsigned POLY = {c.poly:#x}, FCR = {c.fcr}, PRIM = {c.prim}, NR = {c.nr};",
-           f"    static constexpr int NLW = {nlw}, NQD = {nqd}, NPAR = {npar}, NQE = {nqe};",
-           "    // decode: wave Q's leaders (global leader index; -1 = empty slot)",
-           f"    static constexpr int OWN[4][{nlw}] = " + "{" + ", ".join(fmt_list(pad(o, nlw)) for o in own) + "};",
-           f"    static constexpr int SYN[4][{nqd}][4] = " + "{" + ", ".join(
-               "{" + ", ".join("{" + ", ".join(str(seqs[q][4 * qd + j][1]) if 4 * qd + j < len(seqs[q]) else "-1"
-                                               for j in range(4)) + "}" for qd in range(nqd)) + "}"
-               for q in range(4)) + "};",
-           "    template <int Q, int B> static __device__ void dblock(uint32_t (&V)[NLW][8], const uint32_t (&X)[8]);",
-           "    template <int Q, int B> static __device__ void eblock(uint32_t (&V)[NPAR][8], const uint32_t (&X)[8]);",
-           "    template <int Q, class F> static __device__ void depi(const uint32_t (&T)[NLW][8], F &&emit);",
-           "    template <class F> static __device__ void eepi(const uint32_t (&T)[NPAR][8], F &&emit);",
-           "};"]
-    for q in range(4):
-        ws = [(lambda p, l=c.leaders[li]: c.w(l, p)) for li in own[q]]
-        for B in range(32):
-            emit_weight_block(out, f"template <> __device__ __forceinline__ void {st}::dblock<{q}, {B}>("
-                              "uint32_t (&V)[NLW][8], const uint32_t (&X)[8])", ws, B)
-    for q in range(4):
-        js = [j for j in range(npar * q, min(nr, npar * (q + 1)))]
-        ws = [(lambda p, j=j: Gt[p][j] if p < K else 0) for j in js]
-        for B in range((K + 7) // 8):
-            emit_weight_block(out, f"template <> __device__ __forceinline__ void {st}::eblock<{q}, {B}>("
-                              "uint32_t (&V)[NPAR][8], const uint32_t (&X)[8])", ws, B)
-    for q in range(4):
-        emit_fold_epilogue(out, gf, f"{st}_depi{q}", "T", f"{st}::NLW", seqs[q])
-    out.append(f"template <int Q, class F> __device__ __forceinline__ void {st}::depi("
-               "const uint32_t (&T)[NLW][8], F &&emit) {")
-    out.append("    " + " else ".join(f"if constexpr (Q == {q}) {st}_depi{q}(T, emit);" for q in range(4)))
-    out.append("}")
-    # encode: fold only (no expansion); "syndromes" = the wave's parity outputs 0..NPAR-1
-    emit_fold_epilogue(out, gf, f"{st}_eepi", "T", f"{st}::NPAR", [(j, j, 0) for j in range(npar)])
-    out.append(f"template <class F> __device__ __forceinline__ void {st}::eepi("
-               "const uint32_t (&T)[NPAR][8], F &&emit) {")
-    out.append(f"    {st}_eepi(T, emit);")
-    out.append("}")
-    return "\n".join(out)
 
 
 # ---- tile kernel (k_pt): 8 waves share one 256-codeword tile ------------------------------------
@@ -1274,10 +566,9 @@ def main(dst=None):
             "__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {",
             "    return (m & a) | (~m & b);", "}"]
     for cd in CODECS:
-        body.append(gen_codec(PsCodec(*cd)))
-        body.append(gen_pw(PsCodec(*cd)))
-        body.append(gen_py(PsCodec(*cd)))
-        body.append(gen_pt(PsCodec(*cd)))
+        c = PsCodec(*cd)
+        body.append(gen_parity(c))
+        body.append(gen_pt(c))
 
     body.append("#define EZRS_PS_CODEC_LIST(X) \\")
     for i, cd in enumerate(CODECS):

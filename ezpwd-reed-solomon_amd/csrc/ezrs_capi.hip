@@ -219,6 +219,14 @@ int ezrs_destroy(ezrs_codec *c) {
     return 0;
 }
 
+int ezrs_kernel_path(const ezrs_codec *c) {
+    if (!c) return -EINVAL;
+    if (c->ps_id >= 0) return EZRS_PATH_PLANESLICE;
+    if (c->wide_id >= 0) return EZRS_PATH_WIDE;
+    if (c->bs_id >= 0) return EZRS_PATH_BITSLICE;
+    return EZRS_PATH_GENERIC;
+}
+
 int ezrs_get_info(const ezrs_codec *c, ezrs_info *info) {
     if (!c || !info) return -EINVAL;
     const CodecMath &m = c->math;

@@ -8,34 +8,31 @@
 // computes the parity of encode_symbols (rs_base:1296-1332) directly from the data symbols.
 //
 // Arithmetic (codegen/gen_ps.py has the derivation): a 32-bit word holds one position of four
-// codewords, bit 8k + b = bit-plane b of codeword k.  Each bit is a GF(2) stream.
-//   * decode: only one root per cyclotomic coset ("leader") is evaluated -- V_{b,2e} = V_{b,e}^2 --
-//     and the per-plane values are expanded and folded into syndromes (S = sum_b alpha^b V_b) once
-//     per tile: 16 leaders x 8 bits for RS(255,223);
-//   * encode: parity_j = sum_b alpha^b P_{b,j}, P_{b,j} = sum_p bit_b(d_p) G[p][j] with the
-//     systematic generator weights G[p][j] = sum_i Vinv[j][i] alpha^(e_i (N-1-p)): no syndromes,
-//     no parity pass, no workspace.
+// codewords, bit 8k + b = bit-plane b of codeword k.  Each bit is a GF(2) stream.  Only one root per
+// cyclotomic coset ("leader") is evaluated -- V_{b,2e} = V_{b,e}^2 -- and the per-plane values are
+// expanded and folded into syndromes (S = sum_b alpha^b V_b) once per tile: 16 leaders x 8 bits
+// for RS(255,223).  Encode evaluates the syndromes of the data positions; k_ps_parity8 maps them to
+// parity (parity = V^-1 S, bit-sliced over 32 codewords per lane).
 //
-// Tile kernel k_pt (the default): one 512-thread workgroup (8 waves) per 256-codeword tile, two
-// workgroups per CU (80 KiB of LDS each, <= 128 VGPRs: 4 waves per SIMD), persistent over tiles.
-//   * The tile lands in LDS as two 32 KiB half images (positions 0..127, 128..255) by LDS-DMA of
-//     whole 128-byte row chunks (8 lanes per row, 8 rows per instruction) in an XOR-swizzled
-//     layout that makes every ds_read_b128 of the compute conflict-free.  The halves are
-//     pipelined: the next tile's half 0 is fetched while this tile's half 1 is computed, its half 1
-//     while this tile's epilogue runs.
-//   * Waves split the items (decode: leaders; encode: parity symbols, 8 state words each) into GN
-//     groups and the positions into QN = 8 / GN parts; lane l owns codewords l + 64k, k = 0..3 (byte
-//     k of its words).  Piece reads are software-pipelined (the next piece's ds_reads are in flight
-//     while the current one's second block runs).
-//   * A recursive-halving exchange through the consumed half-1 image (plus 16 KiB) leaves every
-//     wave the totals of the items its generated epilogue folds: decode, 4 syndromes (one quad) per
-//     wave; encode, 4 parity symbols per wave, stored straight into the codeword rows.
+// Tile kernel k_pt_lin: one 512-thread workgroup (8 waves) per 256-codeword tile, two workgroups per
+// CU (80 KiB of LDS each, <= 128 VGPRs: 4 waves per SIMD), persistent over tiles.
+//   * The tile's rows are one contiguous span of HBM; 1 KiB LDS-DMA instructions copy it to LDS as it
+//     lies (every line fetched once), the next tile's while this tile's epilogue runs.  Lane l owns
+//     rows 4l .. 4l+3 (byte k of its words = row 4l + k); with an odd pitch the row starts fall in 32
+//     distinct banks, so the row reads (4-byte aligned, then v_alignbyte) are conflict-free.
+//   * Waves split the leaders into GN groups and the 16-position pieces into QN = 8 / GN quarters;
+//     every quarter runs quarter 0's networks and then multiplies its partials by alpha^(-16 q e).
+//   * A recursive-halving exchange through the consumed image leaves every wave the totals of the
+//     leaders its generated epilogue folds: 4 syndromes (one quad) per wave.
+//   * Shard batches (SH): per-row offsets and pads come from a per-tile row table; the bytes before a
+//     shortened row's own pad (the previous row's, in the linear image) are masked off.
 //   * All LDS traffic, LDS-DMA and global stores are inline asm with counted s_waitcnt: the
-//     compiler would otherwise wait for every DMA in flight at each LDS access or barrier.  Stores
-//     and DMAs are issued unconditionally (out-of-range buffer offsets drop unwanted ones), so
-//     every vmcnt is a compile-time constant.
+//     compiler would otherwise wait for every DMA in flight at each LDS access or barrier.
+//   * Measured and dropped: a row-pitched, swizzled image gathered by unaligned per-lane LDS-DMA
+//     (conflict-free aligned ds_read_b128, no v_alignbyte) -- encode 0.177 / decode 0.139 ms per
+//     1 M-codeword call against 0.143 / 0.109 for the linear image; the parity pass fused into this
+//     kernel every 8 tiles (workgroups reach it in lockstep, nothing overlaps it: 0.143 vs 0.144 ms).
 //
-// k_py_syndromes + k_ps_parity8 (EZRS_PS_VARIANT=pair) are the round-2 kernels, kept for A/B runs.
 #include "ezrs_internal.hpp"
 #include "gen/ezrs_ps_tables.inc"
 
@@ -52,16 +49,12 @@ typedef __attribute__((address_space(3))) void lds_void;
 #define EZRS_PT_PRIO 0
 #endif
 #ifdef EZRS_PS_STAMPS
-__device__ unsigned long long g_py_stamps[16][2][8][8];  // [wg][wave][tile][phase]
-#define PY_STAMP(ph) do { __builtin_amdgcn_sched_barrier(0); if (blockIdx.x < 16 && it < 8 && lane == 0) \
-    g_py_stamps[blockIdx.x][Q][it][ph] = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
 // tools/micro/pt_stamps.hip: phase stamps of the linear tile kernel, [wg][wave][tile][phase]
 __device__ unsigned long long g_pt_stamps[16][8][8][8];
 #define PT_STAMP(ph) do { __builtin_amdgcn_sched_barrier(0); if (blockIdx.x < 16 && pt_it < 8 && \
     __lane_id() == 0) g_pt_stamps[blockIdx.x][pt_w][pt_it][ph] = __builtin_amdgcn_s_memtime(); \
     __builtin_amdgcn_sched_barrier(0); } while (0)
 #else
-#define PY_STAMP(ph) do { } while (0)
 #define PT_STAMP(ph) do { } while (0)
 #endif
 
@@ -72,14 +65,9 @@ struct PsArgs {
     uint32_t ncw;               // codewords
     uint32_t ntiles;
     int lo;                     // full-frame position of the rows' first byte (the pad)
-    int hi;                     // one past the last evaluated position (255 decode, 255-NR encode)
-    const uint32_t *neras;      // decode: erasure counts (nullable)
     int32_t *result;            // decode
-    uint8_t *ws;                // decode: [ncw][32] flagged syndromes; pair encode: [NR][ws_pitch]
-    size_t ws_pitch;            // pair encode: codewords per syndrome row (a multiple of 2048)
-    uint8_t *parity;            // tile encode: parity of codeword k at parity + k * pstride
-    uint32_t pstride;
-    uint32_t pspan;             // bytes writable from parity
+    uint8_t *ws;                // decode: [ncw][32] flagged syndromes; encode: [NR][ws_pitch]
+    size_t ws_pitch;            // encode: codewords per syndrome row (a multiple of 2048)
     uint32_t srows;             // shard batches (Shards): codewords per shard, 0 = a plain batch
     int stail_lo;               // full-frame position of a shard's last row's first byte
     uint32_t spitch;            // shard pitch in bytes
@@ -122,7 +110,7 @@ __device__ __forceinline__ void transpose4x4(const uint32_t (&a)[4], uint32_t *o
     out[3] = __builtin_amdgcn_perm(u23, u01, 0x07060302u);
 }
 
-// ---- helpers of the gather-layout kernels ------------------------------------------------------
+// ---- LDS and buffer-resource helpers ----------------------------------------------------------
 __device__ __forceinline__ uint32_t lds_addr(const uint8_t *p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t *)p;
 }
@@ -138,294 +126,6 @@ __device__ __forceinline__ pw_rsrc_t pw_rsrc(const uint8_t *base, uint32_t span)
     r.z = __builtin_amdgcn_readfirstlane((int)span);
     r.w = 0x00020000;
     return r;
-}
-
-// ---- pair-wave syndromes ---------------------------------------------------------------------
-// Two waves (one workgroup, 4 per CU) own a tile of 256 codewords (lane l: rows l + 64k, byte k
-// of its words) and
-// stream it through ONE 32 KiB LDS window of 128 positions x 256 rows.  Full 128-byte row chunks
-// per DMA instruction (8 lanes per row, 8 rows per instruction) keep the gather at line
-// granularity (narrow per-row pieces -- a per-wave design with 32-position windows -- measured
-// 1.5-1.8 TB/s for the fetch alone: tools/micro/pw_dma.hip).  Wave q
-// evaluates ALL leaders over the 16-position pieces p = q, q+2, q+4, q+6 of every window (an even
-// split for any codec length) with the blocks of those positions (no fixups), then the waves swap
-// the partials of the leaders the other owns and each folds its own leaders' syndromes (generated
-// PY_ epilogues).
-//
-// LDS layout: instruction (k, m) (k = byte in word, m = lane block) covers the 8 consecutive rows
-// 64k + l, l = 8m..8m+7, at (8k + m) KiB; lane j of it loads row 64k + l, l = 8m + j/8, 16-byte
-// piece p = (j & 7) ^ f(l), f(l) = (l >> 1) & 7, so piece p of row 64k + l sits at
-//   (8k + l/8) KiB + 128 (l & 7) + 16 (p ^ f(l)):
-// the XOR swizzle makes every 16-lane group of a ds_read_b128 hit 16 distinct bank quads.
-// Encode leaves the syndromes in tile-lane order (workspace column tile*256 + 4l + k holds
-// codeword tile*256 + 64k + l); k_ps_parity<C, true> undoes it.
-constexpr int kPyWin = 128;                                 // positions per window
-constexpr int kPyWinBytes = kTile * kPyWin;                 // 32 KiB
-
-template <class C, bool ENC, int Q>
-__device__ __forceinline__ void py_body(const PsArgs &a, uint8_t *buf, uint32_t (*flags)[64], int lane) {
-    constexpr int NL = C::NL, NLW = C::NLW;
-    constexpr int HI = ENC ? kN - C::NR : kN;                   // one past the last position
-    constexpr int W_HI = (HI - 1) / kPyWin;
-    const int w_lo = a.lo / kPyWin;
-    const pw_rsrc_t rsrc = pw_rsrc(a.base, a.span);
-    const uint32_t lbuf = __builtin_amdgcn_readfirstlane(lds_addr(buf));
-    // Per-lane DMA and LDS-read offsets are recomputed where they are used, from a laundered lane
-    // id (an empty volatile asm the compiler cannot hoist), so that they do not occupy registers
-    // across the 128-word state.
-    auto fresh_lane = [&]() { uint32_t l = (uint32_t)lane; asm volatile("" : "+v"(l)); return l; };
-    // DMA role: this wave issues instructions k = 2Q, 2Q+1, m = 0..7; lane j -> row 64k + 8m + j/8,
-    // piece (j & 7) ^ f(8m + j/8), and (8m + j/8) >> 1 & 7 only depends on m & 1
-    auto doff = [&](uint32_t l, int kk, int mp) {
-        const uint32_t dslot = l >> 3;
-        const uint32_t p = (l & 7) ^ ((4 * mp + (dslot >> 1)) & 7);
-        return (64 * (2 * Q + kk) + dslot) * a.stride + 16 * p;
-    };
-    const uint32_t m_step = 8u * a.stride;                      // rows 64k + l, l += 8
-    // read role: piece p = 2 pp + Q of row 64k + lane at rd(pp) + 8 KiB k
-    auto rd = [&](uint32_t l, int pp) {
-        return 1024 * (l >> 3) + 128 * (l & 7) + 16 * ((2 * pp + Q) ^ ((l >> 1) & 7));
-    };
-    const uint32_t tile_bytes = a.stride * kTile;
-
-    // (LDS-DMA and the window's LDS reads are inline asm, as in the per-wave kernel: the compiler
-    // would otherwise wait for every outstanding vector memory operation in front of each LDS read)
-    auto issue = [&](uint32_t toff, int w) {
-        const uint32_t base = toff + (uint32_t)(kPyWin * w - a.lo);
-        const uint32_t l = fresh_lane();
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-            const uint32_t d0 = base + doff(l, kk, 0), d1 = base + doff(l, kk, 1);
-#pragma unroll
-            for (int m = 0; m < 8; ++m)
-                asm volatile("s_mov_b32 m0, %0\n\t"
-                             "s_nop 0\n\t"
-                             "buffer_load_dwordx4 %1, %2, 0 offen lds"
-                             :: "s"(lbuf + (8 * (2 * Q + kk) + m) * 1024), "v"((m & 1 ? d1 : d0) + m * m_step),
-                                "s"(rsrc) : "memory", "m0");
-        }
-    };
-    // Fix-ups of this wave's pieces (the reader patches what it reads, after the window landed):
-    // pieces straddling the span's start/end come back all-zero; positions before lo hold the
-    // previous row's bytes.
-    auto fix = [&](uint32_t toff, int w) {
-#pragma unroll 1
-        for (int i = 0; i < 16; ++i) {
-            const int k = i >> 2, pp = i & 3;
-            const int64_t r0 = (int64_t)toff + (int64_t)(64 * k + lane) * a.stride;
-            const int64_t o = r0 + kPyWin * w + 16 * (2 * pp + Q) - a.lo;
-            const bool straddle = (o < 0 && o > -16) || (o < (int64_t)a.span && o + 16 > (int64_t)a.span);
-            if (!straddle && o >= r0) continue;
-            const uint32_t dst = lbuf + rd(lane, pp) + 8192 * k;
-#pragma unroll 1
-            for (int j = 0; j < 16; ++j) {
-                const int64_t g = o + j;
-                uint32_t v = 0;
-                if (g >= r0 && !straddle) continue;                // the DMA'd byte stands
-                if (g >= r0 && g < (int64_t)a.span)                // (asm: see pw_fix)
-                    asm volatile("global_load_ubyte %0, %1, off\n\ts_waitcnt vmcnt(0)"
-                                 : "=&v"(v) : "v"(a.base + g) : "memory");
-                asm volatile("ds_write_b8 %0, %1\n\ts_waitcnt lgkmcnt(0)" :: "v"(dst + j), "v"(v) : "memory");
-            }
-        }
-    };
-
-    // deferred stores of the previous tile (issued once the next tile's first window landed):
-    // encode its syndromes, decode its results (flagged codewords' syndromes go out at once)
-    uint32_t pend[ENC ? C::NQW : 1][4];
-    size_t pend_cw0 = 0, pend_col = 0;
-    uint32_t pend_fl = 0;
-    bool pending = false;
-    auto flush = [&]() {
-        if (!pending) return;
-        if constexpr (ENC) {
-            uint8_t *dst = a.ws + pend_col;
-#pragma unroll
-            for (int qd = 0; qd < C::NQW; ++qd)
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) {
-                    const int si = C::SYN[Q][qd][jj];
-                    if (si >= 0) *reinterpret_cast<uint32_t *>(dst + (size_t)si * a.ws_pitch) = pend[qd][jj];
-                }
-        } else {
-            if (Q == 0) {
-                int32_t res[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) res[k] = (pend_fl >> k & 1) ? kSentinel : 0;
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if (pend_cw0 + 64 * k < a.ncw) a.result[pend_cw0 + 64 * k] = res[k];
-            }
-        }
-        pending = false;
-    };
-
-    uint32_t tile = blockIdx.x;
-    if (tile < a.ntiles) issue(tile * tile_bytes, w_lo);
-    for (int it = 0; tile < a.ntiles; tile += gridDim.x, ++it) {
-        (void)it;
-        PY_STAMP(0);
-        const uint32_t toff = tile * tile_bytes;
-        uint32_t V[NL][8];
-#pragma unroll
-        for (int s = 0; s < NL; ++s)
-#pragma unroll
-            for (int t = 0; t < 8; ++t) V[s][t] = 0;
-        static_for<0, W_HI + 1>([&](auto Wc) {
-            constexpr int W = decltype(Wc)::value;
-            if (W < w_lo) return;                                // wave-uniform
-            if (W > w_lo) issue(toff, W);                        // the window buffer is free
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();                                     // window W landed (both waves)
-            PY_STAMP(1 + 2 * W);
-            if (W == w_lo) flush();
-            if (__builtin_expect(kPyWin * W - a.lo < 0 ||
-                                 (int64_t)toff + tile_bytes + kPyWin * W - a.lo + kPyWin > (int64_t)a.span, 0))
-                fix(toff, W);
-            static_for<0, 4>([&](auto Pc) {
-                constexpr int pp = decltype(Pc)::value;
-                constexpr int p16 = kPyWin * W + 16 * (2 * pp + Q); // first position of the piece
-                if constexpr (p16 < HI) {
-                    uint4 R[4];
-                    asm volatile("ds_read_b128 %0, %4\n\t"
-                                 "ds_read_b128 %1, %4 offset:8192\n\t"
-                                 "ds_read_b128 %2, %4 offset:16384\n\t"
-                                 "ds_read_b128 %3, %4 offset:24576\n\t"
-                                 "s_waitcnt lgkmcnt(0)"
-                                 : "=&v"(R[0]), "=&v"(R[1]), "=&v"(R[2]), "=&v"(R[3])
-                                 : "v"(lbuf + rd(fresh_lane(), pp)) : "memory");
-                    uint32_t X[16];
-                    {
-                        const uint32_t c0[4] = {R[0].x, R[1].x, R[2].x, R[3].x};
-                        const uint32_t c1[4] = {R[0].y, R[1].y, R[2].y, R[3].y};
-                        const uint32_t c2[4] = {R[0].z, R[1].z, R[2].z, R[3].z};
-                        const uint32_t c3[4] = {R[0].w, R[1].w, R[2].w, R[3].w};
-                        transpose4x4(c0, X);
-                        transpose4x4(c1, X + 4);
-                        transpose4x4(c2, X + 8);
-                        transpose4x4(c3, X + 12);
-                    }
-                    static_for<0, 2>([&](auto Bc) {
-                        constexpr int p0 = p16 + 8 * decltype(Bc)::value;
-                        if constexpr (p0 < HI) {
-                            uint32_t Y[8];
-#pragma unroll
-                            for (int t = 0; t < 8; ++t) Y[t] = p0 + t < HI ? X[p0 - p16 + t] : 0u;
-                            C::template block<p0 / 8>(V, Y);
-                        }
-                    });
-                }
-            });
-            __syncthreads();                                     // both waves are done with the window
-            PY_STAMP(2 + 2 * W);
-        });
-        // swap partials through the (free) window buffer: wave Q sends the leaders the other owns
-        {
-            uint4 *x = reinterpret_cast<uint4 *>(buf);
-#pragma unroll
-            for (int i = 0; i < NLW; ++i)
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int s = C::OWN[Q ^ 1][i];
-                    x[((Q * NLW + i) * 2 + h) * 64 + lane] =
-                        make_uint4(V[s][4 * h], V[s][4 * h + 1], V[s][4 * h + 2], V[s][4 * h + 3]);
-                }
-        }
-        __syncthreads();
-        uint32_t T[NLW][8];
-        {
-            const uint4 *x = reinterpret_cast<const uint4 *>(buf);
-#pragma unroll
-            for (int i = 0; i < NLW; ++i)
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int s = C::OWN[Q][i];
-                    const uint4 v = x[(((Q ^ 1) * NLW + i) * 2 + h) * 64 + lane];
-                    T[i][4 * h] = V[s][4 * h] ^ v.x;
-                    T[i][4 * h + 1] = V[s][4 * h + 1] ^ v.y;
-                    T[i][4 * h + 2] = V[s][4 * h + 2] ^ v.z;
-                    T[i][4 * h + 3] = V[s][4 * h + 3] ^ v.w;
-                }
-        }
-        __syncthreads();                                         // the exchange area is read
-        PY_STAMP(5);
-        if (tile + gridDim.x < a.ntiles) issue(toff + gridDim.x * tile_bytes, w_lo);
-        const size_t cw0 = (size_t)tile * kTile + lane;          // byte k <-> codeword cw0 + 64k
-        uint32_t nz = 0;
-        uint32_t D[C::NQW][4];
-        C::template epilogue<Q>(T, [&](auto Qc, uint32_t (&Qw)[8]) {
-            constexpr int qd = decltype(Qc)::value;
-            if constexpr (!ENC) {
-                uint32_t vm = 0;
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj)
-                    if (C::SYN[Q][qd][jj] >= 0) vm |= 0x01010101u << jj;
-#pragma unroll
-                for (int t = 0; t < 8; ++t) nz |= Qw[t] & vm;
-            }
-            transpose8(Qw);
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj) D[qd][jj] = Qw[jj];
-        });
-        if constexpr (ENC) {
-#pragma unroll
-            for (int qd = 0; qd < C::NQW; ++qd)
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) pend[qd][jj] = D[qd][jj];
-        }
-        pend_cw0 = cw0;
-        pend_col = (size_t)tile * kTile + 4 * lane;
-        pending = true;
-        PY_STAMP(6);
-        if constexpr (!ENC) {
-            uint32_t fl = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (nz >> (8 * k) & 0xFF) fl |= 1u << k;
-            // OR with the other wave's flags (asm: the compiler would wait for the DMA in flight)
-            const uint32_t fa = lds_addr(reinterpret_cast<uint8_t *>(&flags[Q][lane]));
-            const uint32_t fb = lds_addr(reinterpret_cast<uint8_t *>(&flags[Q ^ 1][lane]));
-            asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" :: "v"(fa), "v"(fl) : "memory");
-            __syncthreads();
-            uint32_t fo;
-            asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(fo) : "v"(fb) : "memory");
-            fl |= fo;
-            if (a.neras) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if (cw0 + 64 * k < a.ncw && a.neras[cw0 + 64 * k]) fl |= 1u << k;
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (cw0 + 64 * k >= a.ncw) fl &= ~(1u << k);
-            pend_fl = fl;
-            if (fl) {                                            // flagged: syndromes for the error path
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    if (!(fl >> k & 1)) continue;
-                    uint8_t *dst = a.ws + (cw0 + 64 * k) * 32;
-#pragma unroll
-                    for (int qd = 0; qd < C::NQW; ++qd)
-#pragma unroll
-                        for (int jj = 0; jj < 4; ++jj) {
-                            const int si = C::SYN[Q][qd][jj];
-                            if (si >= 0) dst[si] = (uint8_t)(D[qd][jj] >> (8 * k));
-                        }
-                }
-            }
-        }
-    }
-    flush();
-}
-
-template <class C, bool ENC>
-__global__ void __attribute__((amdgpu_flat_work_group_size(128, 128), amdgpu_waves_per_eu(2)))
-k_py_syndromes(PsArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t buf[kPyWinBytes];
-    __shared__ uint32_t flags[2][64];
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (wave == 0) py_body<C, ENC, 0>(a, buf, flags, lane);
-    else py_body<C, ENC, 1>(a, buf, flags, lane);
 }
 
 // Bytes s of a[0..3] -> one dword (a[0] in byte 0).
@@ -874,7 +574,7 @@ constexpr int kParCw = 32 * kParGroups;
 
 // 8-wave form of k_ps_parity: wave P computes parity symbols 4P..4P+3 (q_pass4), halving each
 // wave's share of the map and doubling the waves that hide the phases' latencies.
-template <class C, bool PERM>
+template <class C>
 __global__ void __launch_bounds__(512) k_ps_parity8(const uint8_t *ws, size_t ws_pitch, uint8_t *parity,
                                                     size_t pstride, size_t ncw, Shards sh, unsigned len) {
     constexpr int NR = C::NR;
@@ -930,7 +630,7 @@ __global__ void __launch_bounds__(512) k_ps_parity8(const uint8_t *ws, size_t ws
     const size_t cwb = g0 * 32;
     for (int r = threadIdx.x; r < kParCw; r += 512) {
         const size_t x = cwb + r;
-        const size_t k = PERM ? ((x & ~(size_t)255) | ((x & 3) << 6) | ((x >> 2) & 63)) : x;
+        const size_t k = x;
         if (k >= ncw) continue;
         unsigned rlen;
         // shard batches: parity is the base of the rows, each row's parity after its data
@@ -964,32 +664,12 @@ template <class C> bool ps_matches(const DevCodec &d) {
            d.poly == C::POLY;
 }
 
-// Kernels: 0 = tile kernel k_pt (default); 1 = the round-2 pair syndrome kernel + k_ps_parity8
-// (EZRS_PS_VARIANT=pair, comparison runs only).
-int ps_variant() {
-    static const int v = [] {
-        const char *e = getenv("EZRS_PS_VARIANT");
-        return (e && std::string(e) == "pair") ? 1 : 0;
-    }();
-    return v;
-}
-
-// Workgroups per launch (persistent over tiles): tile kernel 2 per CU (80 KiB LDS each), pair
-// kernel 4 per CU (32 KiB each).
-unsigned syn_grid(const DevCodec &d, uint32_t ntiles, int var) {
-    const uint32_t per_cu = var == 0 ? 2u : 4u;
-    const uint32_t nwg = per_cu * (uint32_t)(d.ncu > 0 ? d.ncu : 256);
+// Workgroups per launch (persistent over tiles): 2 per CU (80 KiB LDS each).
+unsigned syn_grid(const DevCodec &d, uint32_t ntiles) {
+    const uint32_t nwg = 2u * (uint32_t)(d.ncu > 0 ? d.ncu : 256);
     return ntiles < nwg ? ntiles : nwg;
 }
 
-#define EZRS_PS_TRIPLE(C)                                                                         \
-    struct T_##C {                                                                                \
-        using PS = ps::PS_##C;                                                                    \
-        using PY = ps::PY_##C;                                                                    \
-        using PT = ps::PT_##C;                                                                    \
-    };
-EZRS_PS_CODEC_LIST(EZRS_PS_TRIPLE)
-#undef EZRS_PS_TRIPLE
 
 } // namespace
 
@@ -1031,12 +711,12 @@ static bool ps_shards_ok(const Shards &g, size_t stride) {
 }
 
 bool ps_can_encode(const DevCodec &, const EncodeArgs &a) {
-    if (a.sh.rows) return a.data_stride <= 256 && ps_variant() == 0 && ps_shards_ok(a.sh, a.data_stride);
+    if (a.sh.rows) return a.data_stride <= 256 && ps_shards_ok(a.sh, a.data_stride);
     return a.data_stride >= 1 && a.data_stride <= 256;
 }
 
 bool ps_can_decode(const DevCodec &d, const DecodeArgs &a) {
-    if (a.sh.rows) return a.data_stride <= 256 && ps_variant() == 0 && ps_shards_ok(a.sh, a.data_stride);
+    if (a.sh.rows) return a.data_stride <= 256 && ps_shards_ok(a.sh, a.data_stride);
     const bool inline_par = a.parity == static_cast<char *>(a.data) + a.len && a.parity_stride == a.data_stride;
     return inline_par && a.data_stride <= 256 && a.data_stride >= a.len + d.nroots;
 }
@@ -1044,7 +724,6 @@ bool ps_can_decode(const DevCodec &d, const DecodeArgs &a) {
 hipError_t launch_ps_encode(int id, const DevCodec &d, const EncodeArgs &a, void *ws, hipStream_t s) {
     const size_t pitch = a.data_stride > a.parity_stride ? a.data_stride : a.parity_stride;
     const size_t maxr = a.sh.rows ? ps_max_rows_shards(a.sh) : ps_max_rows(pitch);
-    const int var = ps_variant();
     for (size_t k0 = 0; k0 < a.ncw; k0 += maxr) {
         const size_t n = a.ncw - k0 < maxr ? a.ncw - k0 : maxr;
         ps::PsArgs p{};
@@ -1062,36 +741,25 @@ hipError_t launch_ps_encode(int id, const DevCodec &d, const EncodeArgs &a, void
         p.ncw = (uint32_t)n;
         p.ntiles = (uint32_t)((n + ps::kTile - 1) / ps::kTile);
         p.lo = (int)(d.load - a.len);              // leading zero positions of a shortened code
-        p.hi = (int)d.load;                        // data positions only
         // shard batches: the parity kernel finds each row's parity from the rows' base
         uint8_t *par = a.sh.rows ? const_cast<uint8_t *>(p.base) : static_cast<uint8_t *>(a.parity) + k0 * a.parity_stride;
-        p.parity = par;
-        p.pstride = (uint32_t)a.parity_stride;
-        p.pspan = (uint32_t)((n - 1) * a.parity_stride + d.nroots);
         p.ws = static_cast<uint8_t *>(ws);
         p.ws_pitch = ps_pitch(n);
         p.ablate = pt_ablate();
-        const unsigned grid = syn_grid(d, p.ntiles, var);
+        const unsigned grid = syn_grid(d, p.ntiles);
         int k = 0;
 #define EZRS_PS_ENC(C)                                                                            \
         if (k++ == id) {                                                                          \
             const unsigned pgrid = (unsigned)((n + ps::kParCw - 1) / ps::kParCw);                 \
-            if (var == 0) {                                                                       \
-                if (a.sh.rows)                                                                    \
-                    hipLaunchKernelGGL((ps::pt::k_pt_lin<ps::PT_##C, true, true>), dim3(grid),    \
-                                       dim3(ps::pt::kThreads), 0, s, p);                          \
-                else                                                                              \
-                    hipLaunchKernelGGL((ps::pt::k_pt_lin<ps::PT_##C, true, false>), dim3(grid),   \
-                                       dim3(ps::pt::kThreads), 0, s, p);                          \
-                hipLaunchKernelGGL((ps::k_ps_parity8<ps::PS_##C, false>), dim3(pgrid), dim3(512), 0, s, \
-                                   static_cast<const uint8_t *>(ws), p.ws_pitch, par, a.parity_stride, n, \
-                                   a.sh, a.len);                                                  \
-            } else {                                                                              \
-                hipLaunchKernelGGL((ps::k_py_syndromes<ps::PY_##C, true>), dim3(grid), dim3(128), 0, s, p); \
-                hipLaunchKernelGGL((ps::k_ps_parity8<ps::PS_##C, true>), dim3(pgrid), dim3(512), 0, s, \
-                                   static_cast<const uint8_t *>(ws), p.ws_pitch, par, a.parity_stride, n, \
-                                   Shards{}, a.len);                                              \
-            }                                                                                     \
+            if (a.sh.rows)                                                                        \
+                hipLaunchKernelGGL((ps::pt::k_pt_lin<ps::PT_##C, true, true>), dim3(grid),        \
+                                   dim3(ps::pt::kThreads), 0, s, p);                              \
+            else                                                                                  \
+                hipLaunchKernelGGL((ps::pt::k_pt_lin<ps::PT_##C, true, false>), dim3(grid),       \
+                                   dim3(ps::pt::kThreads), 0, s, p);                              \
+            hipLaunchKernelGGL((ps::k_ps_parity8<ps::PS_##C>), dim3(pgrid), dim3(512), 0, s,      \
+                               static_cast<const uint8_t *>(ws), p.ws_pitch, par, a.parity_stride, n, \
+                               a.sh, a.len);                                                      \
         }
         EZRS_PS_CODEC_LIST(EZRS_PS_ENC)
 #undef EZRS_PS_ENC
@@ -1104,7 +772,6 @@ hipError_t launch_ps_encode(int id, const DevCodec &d, const EncodeArgs &a, void
 hipError_t launch_ps_syndromes(int id, const DevCodec &d, const DecodeArgs &a, uint8_t *syn_ws,
                                hipStream_t s) {
     const size_t maxr = a.sh.rows ? ps_max_rows_shards(a.sh) : ps_max_rows(a.data_stride);
-    const int var = ps_variant();
     for (size_t k0 = 0; k0 < a.ncw; k0 += maxr) {
         const size_t n = a.ncw - k0 < maxr ? a.ncw - k0 : maxr;
         ps::PsArgs p{};
@@ -1122,25 +789,19 @@ hipError_t launch_ps_syndromes(int id, const DevCodec &d, const DecodeArgs &a, u
         p.ncw = (uint32_t)n;
         p.ntiles = (uint32_t)((n + ps::kTile - 1) / ps::kTile);
         p.lo = (int)(d.load - a.len);
-        p.hi = ps::kN;
-        // the tile kernel flags nonzero syndromes only; the error path adds the codewords with
-        // erasures (their syndromes are zero when the result slot holds 0)
-        p.neras = var == 0 ? nullptr : (a.neras ? a.neras + k0 : nullptr);
         p.result = a.result + k0;
         p.ws = syn_ws + k0 * 32;
         p.ablate = pt_ablate();
-        const unsigned grid = syn_grid(d, p.ntiles, var);
+        const unsigned grid = syn_grid(d, p.ntiles);
         int k = 0;
 #define EZRS_PS_SYN(C)                                                                            \
         if (k++ == id) {                                                                          \
-            if (var == 0 && a.sh.rows)                                                            \
+            if (a.sh.rows)                                                                        \
                 hipLaunchKernelGGL((ps::pt::k_pt_lin<ps::PT_##C, false, true>), dim3(grid),       \
                                    dim3(ps::pt::kThreads), 0, s, p);                              \
-            else if (var == 0)                                                                    \
+            else                                                                                  \
                 hipLaunchKernelGGL((ps::pt::k_pt_lin<ps::PT_##C, false, false>), dim3(grid),      \
                                    dim3(ps::pt::kThreads), 0, s, p);                              \
-            else                                                                                  \
-                hipLaunchKernelGGL((ps::k_py_syndromes<ps::PY_##C, false>), dim3(grid), dim3(128), 0, s, p); \
         }
         EZRS_PS_CODEC_LIST(EZRS_PS_SYN)
 #undef EZRS_PS_SYN

@@ -90,6 +90,7 @@ def lib():
         L.ezrs_encode_shards.argtypes = [_vp, _vp, _sz, _sz, _u, _sz, _vp]
         L.ezrs_decode_shards.argtypes = [_vp, _vp, _sz, _sz, _u, _sz, _vp, _sz, _vp, _vp, _vp, _sz,
                                          _vp, _sz, _vp]
+        L.ezrs_kernel_path.argtypes = [_vp]
         L.ezrs_host_alloc.argtypes = [C.POINTER(_vp), _sz]
         L.ezrs_host_free.argtypes = [_vp]
         L.ezbch_last_error.restype = C.c_char_p
@@ -218,6 +219,12 @@ class Codec:
     def torch_dtype(self):
         import torch
         return torch.uint8 if self.dtype == np.uint8 else torch.uint16
+
+    @property
+    def kernel_path(self):
+        """'generic' | 'bitslice' | 'planeslice' | 'wide' (ezrs_kernel_path)."""
+        return ("generic", "bitslice", "planeslice", "wide")[_check(lib().ezrs_kernel_path(self._h),
+                                                                      "ezrs_kernel_path")]
 
     def reserve(self, ncw, stream=None):
         """Pre-size the workspace of `stream` (default: the current torch stream)."""

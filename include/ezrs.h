@@ -81,6 +81,13 @@ int ezrs_create_rs(ezrs_codec **out, unsigned n, unsigned k, int device);
  * FCR = 128 - (255-K)/2, PRIM = 11 (rs:101-104). */
 int ezrs_create_ccsds(ezrs_codec **out, unsigned k, int dual, int device);
 int ezrs_destroy(ezrs_codec *codec);
+/* Which kernel family serves the codec's full-length batches: EZRS_PATH_* (diagnostics; every
+ * family is bit-exact with the reference). */
+#define EZRS_PATH_GENERIC 0     /* per-codeword kernels (lane or 32-lane group per codeword)        */
+#define EZRS_PATH_BITSLICE 1    /* bit-sliced GF(2^8) kernels (CCSDS dual basis)                     */
+#define EZRS_PATH_PLANESLICE 2  /* plane-sliced GF(2^8) tile kernels (RS(255,K), NROOTS <= 32)       */
+#define EZRS_PATH_WIDE 3        /* GF(2^16) remainder-network kernels (RS(65535,65503/65519))        */
+int ezrs_kernel_path(const ezrs_codec *codec);
 int ezrs_get_info(const ezrs_codec *codec, ezrs_info *info);
 
 /* Pre-size the workspace of `stream` (NULL: the null stream) for batches of up to `ncw` codewords,

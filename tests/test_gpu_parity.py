@@ -180,9 +180,11 @@ def _inject(torch, cw, n_err, n_era, nn, gen):
     return locs, eras
 
 
-# the 17 codecs rsvalidate cross-checks against Karn (rsvalidate.C:46-62), plus CCSDS
+# the 17 codecs rsvalidate cross-checks against Karn (rsvalidate.C:46-62), plus CCSDS; every
+# RS(255,K) with NROOTS <= 32 and RS_CCSDS_CONV(255,239) run the plane-sliced tile kernels
 RSVALIDATE_NR = [1, 2, 3, 4, 7, 9, 12, 16, 17, 27, 46, 77, 99, 127, 128, 129, 199]
-BULK = ([("RS(255,223)", 1 << 16), ("RS_CCSDS(255,223)", 1 << 16), ("RS(255,251)", 1 << 16)] +
+BULK = ([("RS(255,223)", 1 << 16), ("RS_CCSDS(255,223)", 1 << 16), ("RS(255,251)", 1 << 16),
+         ("RS_CCSDS_CONV(255,239)", 1 << 14)] +
         [(f"RS(255,{255 - nr})", 1 << 12) for nr in RSVALIDATE_NR if nr not in (4, 32)])
 
 
@@ -190,10 +192,19 @@ BULK = ([("RS(255,223)", 1 << 16), ("RS_CCSDS(255,223)", 1 << 16), ("RS(255,251)
 def test_bulk_vs_oracle(torch, maker, ncw):
     """Random shortened length, error loads 0..3x capacity: every output equals the oracle's
     (result, positions, corrected data and parity); 64k codewords for the headline codecs, 4k for
-    the rest of rsvalidate's set."""
+    the rest of rsvalidate's set.  Codecs with NROOTS <= 32 must be on the plane-sliced path."""
     import ezrs
-    c = ezrs.Codec.rs(255, int(maker[7:-1])) if maker.startswith("RS(") else ezrs.Codec.ccsds(223)
-    oc = O.Codec(*(O.rs_params(255, c.load) if maker.startswith("RS(") else O.ccsds_params(223)))
+    if maker.startswith("RS("):
+        c = ezrs.Codec.rs(255, int(maker[7:-1]))
+        oc = O.Codec(*O.rs_params(255, c.load))
+    elif maker.startswith("RS_CCSDS_CONV"):
+        c = ezrs.Codec.ccsds(239, dual=False)
+        oc = O.Codec(*O.ccsds_params(239, False))
+    else:
+        c = ezrs.Codec.ccsds(223)
+        oc = O.Codec(*O.ccsds_params(223))
+    if c.nroots <= 32 and not c.dual:
+        assert c.kernel_path == "planeslice", (maker, c.kernel_path)
     rng = np.random.default_rng(11)
     L, nr = c.load - 17, c.nroots
     data = rng.integers(0, 256, (ncw, L + nr)).astype(np.uint8)
