@@ -11,6 +11,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -532,6 +533,35 @@ int ezrs_decode_shards(const ezrs_codec *c, void *shards, size_t shard_pitch, si
 // ---- host-memory pipeline ---------------------------------------------------------------------
 namespace {
 
+// Rows whose decode result is nonzero, compacted: ix[0] = count, ix[1 + j] = chunk-relative row
+// index of compacted row j (in no particular order), out + j * row_bytes = its bytes.  ix[0] must be
+// zero on entry.
+__global__ void __launch_bounds__(256) k_compact_rows(const int32_t *result, size_t n, const char *rows,
+                                                      size_t row_bytes, uint32_t *ix, char *out) {
+    __shared__ uint32_t slot[256];
+    const size_t k = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const bool mine = k < n && result[k] != 0;
+    slot[threadIdx.x] = mine ? atomicAdd(ix, 1u) : 0xFFFFFFFFu;
+    if (mine) ix[1 + slot[threadIdx.x]] = (uint32_t)k;
+    __syncthreads();
+    // the block copies its flagged rows, 4 bytes per thread per step
+    for (int t = 0; t < 256; ++t) {
+        const uint32_t sl = slot[t];
+        if (sl == 0xFFFFFFFFu) continue;
+        const char *src = rows + ((size_t)blockIdx.x * 256 + t) * row_bytes;
+        char *dst = out + (size_t)sl * row_bytes;
+        for (size_t b = threadIdx.x; b < row_bytes; b += 256) dst[b] = src[b];
+    }
+}
+
+hipError_t launch_compact_rows(const int32_t *result, size_t n, const char *rows, size_t row_bytes,
+                               uint32_t *ix, char *out, int ncu, hipStream_t st) {
+    (void)ncu;
+    const unsigned grid = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(k_compact_rows, dim3(grid), dim3(256), 0, st, result, n, rows, row_bytes, ix, out);
+    return hipGetLastError();
+}
+
 // Device and pinned-host staging of the host-memory forms: two sets (one per pipeline stream).
 int ensure_stage(ezrs_codec *c, size_t dbytes, size_t hbytes) {
     if (!c->streams[0])
@@ -560,8 +590,31 @@ int ensure_stage(ezrs_codec *c, size_t dbytes, size_t hbytes) {
 
 size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
-size_t default_chunk(size_t row_bytes) {
-    const size_t target = (size_t)64 << 20;  // 64 MiB of staged rows per chunk
+// Host threads for the CPU-side scatters of the host-memory forms (EZRS_HOST_THREADS, default 8).
+size_t host_threads() {
+    static const size_t n = [] {
+        const char *e = getenv("EZRS_HOST_THREADS");
+        const long v = e ? atol(e) : 8;
+        return (size_t)(v < 1 ? 1 : v > 64 ? 64 : v);
+    }();
+    return n;
+}
+
+// Pinned (page-locked) host memory?  Pageable copies go through the runtime's own staging, which
+// pipelines badly on single large copies: they get smaller chunks.
+bool host_pinned(const void *p) {
+    hipPointerAttribute_t at{};
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return at.type == hipMemoryTypeHost;
+}
+
+size_t default_chunk(size_t row_bytes, bool pinned = true) {
+    // staged rows per chunk: 64 MiB from pinned memory, 32 MiB from pageable (measured, 1 M
+    // RS(255,223) rows: pageable decode 17.5 ms at 64 MiB, 6.6 ms at 32 MiB; pinned 5.4 / 6.9)
+    const size_t target = (size_t)(pinned ? 64 : 32) << 20;
     size_t n = target / (row_bytes ? row_bytes : 1);
     return n ? n : 1;
 }
@@ -581,18 +634,32 @@ int encode_host_core(ezrs_codec *c, const char *data, size_t data_stride, unsign
     // below len, 0 included, is legal for one codeword and must not size the staging)
     const size_t drow = ncw == 1 ? need : span ? data_stride : need;
     const bool par_direct = parity_stride == NR || ncw == 1;       // caller's parity is compact
-    if (!chunk) chunk = default_chunk(drow * w);
+    if (!chunk) chunk = default_chunk(drow * w, host_pinned(data));
     if (chunk > ncw) chunk = ncw;
     const size_t b_in = align_up(chunk * drow * w), b_par = align_up(chunk * NR * w),
                  b_ws = align_up(ws_bytes_for(c, chunk));
     const size_t h_in = span ? 0 : align_up(chunk * need * w), h_par = par_direct ? 0 : b_par;
     if (int r = ensure_stage(c, b_in + b_par + b_ws, h_in + h_par + 256)) return r;
     struct Pending { size_t k0 = 0, n = 0; bool live = false; } pend[2];
+    // scatter of a chunk's compact parity into the caller's rows: split over host threads (a
+    // single thread writing 32-byte pieces into 1 M rows takes ~5 ms, 2x the copy itself)
     auto scatter = [&](int s) {
         if (!pend[s].live || par_direct) return;
         const char *src = static_cast<const char *>(c->h_stage[s]) + h_in;
-        for (size_t r = 0; r < pend[s].n; ++r)
-            std::memcpy(parity + (pend[s].k0 + r) * parity_stride * w, src + r * NR * w, NR * w);
+        const size_t n = pend[s].n, k0 = pend[s].k0;
+        auto part = [&](size_t r0, size_t r1) {
+            for (size_t r = r0; r < r1; ++r)
+                std::memcpy(parity + (k0 + r) * parity_stride * w, src + r * NR * w, NR * w);
+        };
+        const size_t nt = n >= 65536 ? host_threads() : 1;
+        if (nt <= 1) {
+            part(0, n);
+            return;
+        }
+        std::vector<std::thread> th;
+        for (size_t t = 1; t < nt; ++t) th.emplace_back(part, n * t / nt, n * (t + 1) / nt);
+        part(0, n / nt);
+        for (auto &x : th) x.join();
     };
     for (size_t i = 0, k0 = 0; k0 < ncw; ++i, k0 += chunk) {
         const int s = (int)(i & 1);
@@ -686,24 +753,59 @@ int ezrs_decode_host(ezrs_codec *c, void *data, size_t data_stride, unsigned len
                                 static_cast<const char *>(data) + (size_t)len * w;
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard g(c->device);
-    // device row: the caller's whole row when parity is inline (one linear copy each way)
+    // device row: the caller's whole row when parity is inline (one linear copy in)
     const size_t row = inline_par ? data_stride * w : (size_t)(len + NR) * w;
-    if (!chunk) chunk = default_chunk(row);
+    if (!chunk) chunk = default_chunk(row, host_pinned(data));
     if (chunk > ncw) chunk = ncw;
     const size_t b_cw = align_up(chunk * row), b_er = align_up(chunk * ecols * 4),
                  b_ne = align_up(neras ? chunk * 4 : 0), b_rs = align_up(chunk * 4),
                  b_ps = align_up(positions ? chunk * NR * 4 : 0),
                  b_co = align_up(corr ? chunk * NR * w : 0),
-                 b_sy = align_up(ws_bytes_for(c, chunk));
-    if (int r = ensure_stage(c, b_cw + b_er + b_ne + b_rs + b_ps + b_co + b_sy, 0)) return r;
+                 b_sy = align_up(ws_bytes_for(c, chunk)),
+                 b_ix = align_up(chunk * 4 + 4), b_cp = align_up(chunk * row);
+    // pinned host staging: the compacted rows and their indices (+ the count)
+    const size_t h_cp = align_up(chunk * row), h_ix = align_up(chunk * 4 + 4);
+    if (int r = ensure_stage(c, b_cw + b_er + b_ne + b_rs + b_ps + b_co + b_sy + b_ix + b_cp, h_cp + h_ix)) return r;
+    // Only the codewords whose result is nonzero can differ from what was sent (a clean codeword is
+    // never written; -1 may leave partial corrections, rs_base:1238-1241): the device compacts those
+    // rows, and only the results and the compacted rows come back.
+    struct Pending { size_t k0 = 0; bool live = false; } pend[2];
+    auto finish = [&](int s) -> int {
+        if (!pend[s].live) return 0;
+        pend[s].live = false;
+        hipStream_t st = c->streams[s];
+        HIP_TRY(hipStreamSynchronize(st));                      // results and the count are back
+        char *hb = static_cast<char *>(c->h_stage[s]);
+        const uint32_t *hix = reinterpret_cast<const uint32_t *>(hb + h_cp);
+        const uint32_t cnt = hix[0];
+        if (!cnt) return 0;
+        char *base = static_cast<char *>(c->d_stage[s]);
+        const char *dix = base + b_cw + b_er + b_ne + b_rs + b_ps + b_co + b_sy, *dcp = dix + b_ix;
+        HIP_TRY(hipMemcpyAsync(hb, dcp, cnt * row, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(hb + h_cp + 4, dix + 4, cnt * 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        const size_t k0 = pend[s].k0;
+        for (uint32_t j = 0; j < cnt; ++j) {
+            const size_t k = k0 + hix[1 + j];
+            const char *src = hb + (size_t)j * row;
+            if (inline_par) {
+                std::memcpy(static_cast<char *>(data) + k * data_stride * w, src, (size_t)(len + NR) * w);
+            } else {
+                std::memcpy(static_cast<char *>(data) + k * data_stride * w, src, (size_t)len * w);
+                std::memcpy(static_cast<char *>(parity) + k * parity_stride * w, src + (size_t)len * w,
+                            (size_t)NR * w);
+            }
+        }
+        return 0;
+    };
     for (size_t i = 0, k0 = 0; k0 < ncw; ++i, k0 += chunk) {
         const int s = (int)(i & 1);
         hipStream_t st = c->streams[s];
         const size_t n = ncw - k0 < chunk ? ncw - k0 : chunk;
-        if (i >= 2) HIP_TRY(hipStreamSynchronize(st));
+        if (int r = finish(s)) return r;                        // chunk i-2 (this stream's buffers)
         char *base = static_cast<char *>(c->d_stage[s]);
         char *dcw = base, *der = dcw + b_cw, *dne = der + b_er, *drs = dne + b_ne, *dps = drs + b_rs,
-             *dco = dps + b_ps, *dsy = dco + b_co;
+             *dco = dps + b_ps, *dsy = dco + b_co, *dix = dsy + b_sy, *dcp = dix + b_ix;
         char *hd = static_cast<char *>(data) + k0 * data_stride * w;
         char *hp = static_cast<char *>(parity) + k0 * parity_stride * w;
         const size_t span = ((n - 1) * data_stride + len + NR) * w;
@@ -711,20 +813,20 @@ int ezrs_decode_host(ezrs_codec *c, void *data, size_t data_stride, unsigned len
             HIP_TRY(hipMemcpyAsync(dcw, hd, span, hipMemcpyHostToDevice, st));
         } else {
             HIP_TRY(ezrs::copy2d(dcw, row, hd, data_stride * w, (size_t)len * w, n,
-                                     hipMemcpyHostToDevice, st));
+                                 hipMemcpyHostToDevice, st));
             HIP_TRY(ezrs::copy2d(dcw + (size_t)len * w, row, hp, parity_stride * w,
-                                     (size_t)NR * w, n, hipMemcpyHostToDevice, st));
+                                 (size_t)NR * w, n, hipMemcpyHostToDevice, st));
         }
         if (eras)
             HIP_TRY(ezrs::copy2d(der, ecols * 4, eras + k0 * eras_stride, eras_stride * 4,
-                                     ecols * 4, n, hipMemcpyHostToDevice, st));
+                                 ecols * 4, n, hipMemcpyHostToDevice, st));
         if (neras) HIP_TRY(hipMemcpyAsync(dne, neras + k0, n * 4, hipMemcpyHostToDevice, st));
         if (positions)
             HIP_TRY(ezrs::copy2d(dps, (size_t)NR * 4, positions + k0 * pos_stride,
-                                     pos_stride * 4, (size_t)NR * 4, n, hipMemcpyHostToDevice, st));
+                                 pos_stride * 4, (size_t)NR * 4, n, hipMemcpyHostToDevice, st));
         if (corr)   // corr is copy-in/copy-out: entries the decode does not write keep their value
             HIP_TRY(ezrs::copy2d(dco, (size_t)NR * w, static_cast<char *>(corr) + k0 * corr_stride * w,
-                                     corr_stride * w, (size_t)NR * w, n, hipMemcpyHostToDevice, st));
+                                 corr_stride * w, (size_t)NR * w, n, hipMemcpyHostToDevice, st));
         const size_t ds = row / w;
         DecodeArgs a{dcw, ds, len, dcw + (size_t)len * w, ds,
                      eras ? reinterpret_cast<uint32_t *>(der) : nullptr, ecols,
@@ -733,23 +835,21 @@ int ezrs_decode_host(ezrs_codec *c, void *data, size_t data_stride, unsigned len
                      positions ? reinterpret_cast<uint32_t *>(dps) : nullptr, NR,
                      corr ? dco : nullptr, NR, n};
         HIP_TRY(dispatch_decode(c, a, reinterpret_cast<uint8_t *>(dsy), st));
-        if (inline_par) {
-            HIP_TRY(hipMemcpyAsync(hd, dcw, span, hipMemcpyDeviceToHost, st));
-        } else {
-            HIP_TRY(ezrs::copy2d(hd, data_stride * w, dcw, row, (size_t)len * w, n,
-                                     hipMemcpyDeviceToHost, st));
-            HIP_TRY(ezrs::copy2d(hp, parity_stride * w, dcw + (size_t)len * w, row,
-                                     (size_t)NR * w, n, hipMemcpyDeviceToHost, st));
-        }
+        HIP_TRY(hipMemsetAsync(dix, 0, 4, st));
+        HIP_TRY(launch_compact_rows(reinterpret_cast<const int32_t *>(drs), n, dcw, row,
+                                    reinterpret_cast<uint32_t *>(dix), dcp, c->dev.ncu, st));
         HIP_TRY(hipMemcpyAsync(result + k0, drs, n * 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(static_cast<char *>(c->h_stage[s]) + h_cp, dix, 4, hipMemcpyDeviceToHost, st));
         if (positions)
             HIP_TRY(ezrs::copy2d(positions + k0 * pos_stride, pos_stride * 4, dps,
-                                     (size_t)NR * 4, (size_t)NR * 4, n, hipMemcpyDeviceToHost, st));
+                                 (size_t)NR * 4, (size_t)NR * 4, n, hipMemcpyDeviceToHost, st));
         if (corr)
             HIP_TRY(ezrs::copy2d(static_cast<char *>(corr) + k0 * corr_stride * w, corr_stride * w,
-                                     dco, (size_t)NR * w, (size_t)NR * w, n, hipMemcpyDeviceToHost, st));
+                                 dco, (size_t)NR * w, (size_t)NR * w, n, hipMemcpyDeviceToHost, st));
+        pend[s] = {k0, true};
     }
-    for (int s = 0; s < 2; ++s) HIP_TRY(hipStreamSynchronize(c->streams[s]));
+    for (int s = 0; s < 2; ++s)
+        if (int r = finish(s)) return r;
     return 0;
 }
 

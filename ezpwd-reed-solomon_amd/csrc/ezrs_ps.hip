@@ -31,7 +31,9 @@
 //   * Measured and dropped: a row-pitched, swizzled image gathered by unaligned per-lane LDS-DMA
 //     (conflict-free aligned ds_read_b128, no v_alignbyte) -- encode 0.177 / decode 0.139 ms per
 //     1 M-codeword call against 0.143 / 0.109 for the linear image; the parity pass fused into this
-//     kernel every 8 tiles (workgroups reach it in lockstep, nothing overlaps it: 0.143 vs 0.144 ms).
+//     kernel every 8 tiles (workgroups reach it in lockstep, nothing overlaps it: 0.143 vs 0.144 ms);
+//     a persistent parity kernel (one workgroup per CU, planes and row stage in separate LDS, the
+//     next chunk's workspace loads in flight during the map): 0.149 vs 0.144 ms.
 //
 #include "ezrs_internal.hpp"
 #include "gen/ezrs_ps_tables.inc"

@@ -163,8 +163,9 @@ int ezrs_decode_shards(const ezrs_codec *codec, void *shards, size_t shard_pitch
  * Encode sends each chunk's rows to the device (one linear copy of the rows' span when the row
  * pitch is at most about twice the row; otherwise the rows are gathered into pinned staging first)
  * and brings back only the parity, as one compact block that is then scattered into place: the
- * caller's data symbols are never written.  Decode copies inline-parity rows as one linear span
- * each way. */
+ * caller's data symbols are never written.  Decode sends inline-parity rows as one linear span;
+ * back come the results and only the rows whose result is nonzero (compacted on the device, then
+ * scattered into place): a clean codeword's row is never written. */
 int ezrs_encode_host(ezrs_codec *codec, const void *data, size_t data_stride, unsigned len,
                      void *parity, size_t parity_stride, size_t ncw, size_t chunk);
 int ezrs_encode_rows_host(ezrs_codec *codec, void *rows, size_t stride, unsigned len, size_t ncw,

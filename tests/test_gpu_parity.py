@@ -127,6 +127,36 @@ def test_host_pipeline_inline_parity(torch, n, k, pad, pinned):
     np.testing.assert_array_equal(h, exp)
 
 
+@pytest.mark.parametrize("pinned", [False, True])
+def test_host_pipeline_sparse_changes(torch, pinned):
+    """decode_host brings back only the rows whose result is nonzero (compacted on the device):
+    5% of the rows correctable, 1% overwhelmed (partial corrections kept, rs_base:1238-1241), the
+    rest clean, over several chunks and both pipeline streams -- every row and result equals the
+    oracle's."""
+    import ezrs
+    c = ezrs.Codec.rs(255, 223)
+    oc = O.Codec(*O.rs_params(255, 223))
+    rng = np.random.default_rng(77)
+    ncw, stride = 9000, 258
+    host = rng.integers(0, 256, (ncw, stride)).astype(np.uint8)
+    oc.encode_batch(host, 223)
+    pick = rng.random(ncw)
+    for kk in np.nonzero(pick < 0.06)[0]:
+        m = 40 if pick[kk] < 0.01 else int(rng.integers(1, 17))
+        locs = rng.choice(255, m, replace=False)
+        host[kk, locs] ^= rng.integers(1, 256, m).astype(np.uint8)
+    exp = host.copy()
+    exp_r = oc.decode_batch(exp, 223)
+    buf = torch.from_numpy(host)
+    if pinned:
+        buf = buf.pin_memory()
+    h = buf.numpy()
+    r = c.decode_host(h, 223, chunk=1000)
+    np.testing.assert_array_equal(r, exp_r)
+    np.testing.assert_array_equal(h, exp)
+    assert (r == -1).any() and (r > 0).any() and (r == 0).mean() > 0.9
+
+
 @pytest.mark.parametrize("n,k,ncw,L", [(65535, 65503, 6, 65503), (65535, 65503, 40, 900),
                                         (1023, 1001, 300, 1001), (4095, 4063, 50, 2000)])
 def test_wide_symbol_lane_kernels_vs_oracle(torch, n, k, ncw, L):

@@ -235,3 +235,39 @@ def test_wide_multi_pass_batch(torch):
     torch.cuda.synchronize()
     np.testing.assert_array_equal(r.cpu().numpy(), nerr)
     np.testing.assert_array_equal(_host(d), ref)
+
+
+def test_wide_full_length_1k(torch):
+    """C4 shape at 1024 full-length RS(65535,65503) codewords (134 MB): parity, and the decode of
+    8 errors + 4 erasures in every codeword (results, corrected rows, positions), all against the
+    oracle."""
+    c = _codec(65535, 65503, True)
+    oc = O.Codec(*O.rs_params(65535, 65503))
+    ncw, L, nr = 1024, 65503, 32
+    rng = np.random.default_rng(0xC4)
+    host = rng.integers(0, 65536, (ncw, L + nr)).astype(np.uint16)
+    dev = _dev(torch, host)
+    c.encode(dev, L)
+    oc.encode_batch(host, L, nthreads=16)
+    np.testing.assert_array_equal(_host(dev), host)
+    cw = host.copy()
+    eras = np.zeros((ncw, nr), np.uint32)
+    neras = np.full(ncw, 4, np.uint32)
+    for i in range(ncw):
+        locs = rng.choice(L + nr, 12, replace=False)
+        cw[i, locs] ^= rng.integers(1, 65536, 12).astype(np.uint16)
+        eras[i, :4] = locs[8:]
+    exp = cw.copy()
+    exp_pos = np.zeros((ncw, nr), np.uint32)
+    exp_r = oc.decode_batch(exp, L, None, eras, neras, exp_pos, nthreads=16)
+    d = _dev(torch, cw)
+    pos = torch.zeros((ncw, nr), dtype=torch.int32, device="cuda")
+    r = c.decode(d, L, eras=torch.from_numpy(eras.view(np.int32)).cuda(),
+                 neras=torch.from_numpy(neras.view(np.int32)).cuda(), positions=pos)
+    r = r.cpu().numpy()
+    np.testing.assert_array_equal(r, exp_r)
+    assert (r == 12).all()
+    np.testing.assert_array_equal(_host(d), exp)
+    np.testing.assert_array_equal(_host(d), host)
+    got = pos.cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(got[:, :12], exp_pos[:, :12])
