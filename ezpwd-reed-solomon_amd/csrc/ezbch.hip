@@ -19,8 +19,9 @@
 //                   degree 1 directly, degrees 2..4 as an affine GF(2)-linear equation
 //                   A4 y^4 + A2 y^2 + A1 y = delta solved by elimination over the m basis bits,
 //                   degree > 4 by a Chien search over the codeword's bit positions.
-// Device limits: t <= 16 and ecc_bits <= 256 (four 64-bit remainder words); other init_bch-valid
-// codecs are refused with -ENOTSUP at creation.  There is no CPU path.
+//   k_bch_decode_big t <= 64, ecc_bits <= 1024 with run-time t (per-lane arrays).
+//   k_bch_*_wave     every larger init_bch-valid codec: one wavefront per codeword (see below).
+// There is no CPU path.
 #include <hip/hip_runtime.h>
 
 #include <cerrno>
@@ -45,7 +46,8 @@ constexpr int kEBADMSG = 74, kEINVAL = 22;   // Linux errno values, negated as d
 struct DevBch {
     int m, n, t, ecc_bits, ecc_bytes;
     int lds_tabs;             // exp/log tables staged in LDS (m <= 12)
-    int nw;                   // 64-bit words of the remainder (1, 2, 4)
+    int nw;                   // 64-bit words of the remainder (1 .. 16; the wave path: 64 nwl)
+    int nwl;                  // wave path (t > 64 or ecc_bits > 1024): remainder words per lane, else 0
     uint64_t emask[kMaxNW];   // the ecc_bits significant bits of a left-justified remainder
     const uint64_t *step;     // [256][nw] byte-step remainder table
     const uint16_t *ex;       // [2n] alpha^i
@@ -678,7 +680,285 @@ __global__ void __launch_bounds__(kThreads) k_bch_decode_big(DevBch b, BchArgs a
     }
 }
 
+// ---- t > 64 or ecc_bits > 1024: one wavefront per codeword -------------------------------------
+// Every init_bch-valid codec (m <= 15: ecc_bits < 32768) runs here.  The remainder is spread over
+// the wave, lane l holding 64-bit words l*NWL .. l*NWL+NWL-1 of the left-justified remainder; one
+// data byte shifts the whole wave's remainder by 8 bits (the carry from lane l+1 by a lane shuffle)
+// and XORs row fb of the byte-step table [256][64 NWL] (global memory, one coalesced row per byte).
+// Decode: syndromes lane-parallel over the odd indices (from the set bits of the remainder), even
+// ones by one log-table lookup (S_(2^k o) = S_o^(2^k)); binary Berlekamp-Massey with the locator
+// and B in LDS (discrepancy as a wave XOR reduction, updates lane-parallel); roots in closed form
+// for degree <= 4 (as the lane path), else a lane-parallel Chien search over the bit positions;
+// locations rank-sorted ascending.  The per-codeword chains (a byte step, a BM step) are serial,
+// so this path is for correctness over the whole parameter range, not the C5 rate.
+__device__ __forceinline__ uint64_t shfl_down64(uint64_t v, int d) {
+    const uint32_t lo = __shfl_down((uint32_t)v, d, 64), hi = __shfl_down((uint32_t)(v >> 32), d, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+}
+__device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v ^= (uint32_t)__shfl_xor((int)v, d, 64);
+    return v;
+}
+// x mod (2^m - 1) for x < 2^30
+__device__ __forceinline__ uint32_t mod_n(uint32_t x, int m, uint32_t n) {
+    x = (x & n) + (x >> m);
+    x = (x & n) + (x >> m);
+    return x >= n ? x - n : x;
+}
+
+// Remainder of the data bytes p[0..len): w[j] = word lane*NWL + j.
+template <int NWL>
+__device__ void wave_remainder(const DevBch &b, const uint8_t *p, unsigned len, uint64_t (&w)[NWL]) {
+    const int lane = (int)(threadIdx.x & 63);
+#pragma unroll
+    for (int j = 0; j < NWL; ++j) w[j] = 0;
+    const size_t nw = (size_t)64 * NWL;
+    for (unsigned c0 = 0; c0 < len; c0 += 64) {
+        const uint32_t mine = c0 + lane < len ? p[c0 + lane] : 0u;
+        const unsigned cnt = len - c0 < 64u ? len - c0 : 64u;
+        for (unsigned i = 0; i < cnt; ++i) {
+            const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)mine, (int)i);
+            const uint32_t fb = ((uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(w[0] >> 56), 0) ^ v) & 0xffu;
+            const uint64_t nxt = lane == 63 ? 0ull : shfl_down64(w[0], 1);
+            const uint64_t *row = b.step + fb * nw + (size_t)lane * NWL;
+#pragma unroll
+            for (int j = 0; j < NWL; ++j) {
+                const uint64_t lo = j + 1 < NWL ? w[j + 1 < NWL ? j + 1 : j] : nxt;
+                w[j] = ((w[j] << 8) | (lo >> 56)) ^ row[j];
+            }
+        }
+    }
+}
+
+template <int NWL>
+__global__ void __launch_bounds__(64) k_bch_encode_wave(DevBch b, BchArgs a) {
+    const size_t k = blockIdx.x;
+    const int lane = (int)threadIdx.x;
+    uint64_t w[NWL];
+    wave_remainder<NWL>(b, a.data + k * a.dstride, a.len, w);
+    uint8_t *e = a.ecc + k * a.estride;
+#pragma unroll
+    for (int j = 0; j < NWL; ++j) {
+        const int wi = lane * NWL + j;
+        for (int bb = 0; bb < 8; ++bb) {
+            const int i = 8 * wi + bb;
+            if (i < b.ecc_bytes) e[i] = (uint8_t)(w[j] >> (56 - 8 * bb));
+        }
+    }
+}
+
+// Per-wave LDS of the decode: S[0..2t] u16 | C[W] u16 | B[W] u16 | lgC[W] i32 | P[t] u32 | E[t] u32 | cnt
+__host__ __device__ inline size_t wave_w(int t) { return ((size_t)2 * t + 2 + 63) / 64 * 64; }
+__host__ __device__ inline size_t wave_lds_bytes(int t) {
+    return ((size_t)2 * t + 2) * 2 + wave_w(t) * (2 + 2 + 4) + (size_t)t * 8 + 16;
+}
+
+template <int NWL>
+__global__ void __launch_bounds__(64) k_bch_decode_wave(DevBch b, BchArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int T = b.t, lane = (int)threadIdx.x, m = b.m;
+    const uint32_t n = (uint32_t)b.n;
+    const size_t W = wave_w(T);
+    uint16_t *S = reinterpret_cast<uint16_t *>(smem);
+    uint16_t *C = S + 2 * T + 2, *B = C + W;
+    int32_t *lgC = reinterpret_cast<int32_t *>(B + W);
+    uint32_t *P = reinterpret_cast<uint32_t *>(lgC + W), *E = P + T;
+    const GF f{b.ex, b.lg, b.n};
+    const size_t k = blockIdx.x;
+    if (8ull * a.len > (unsigned long long)(b.n - b.ecc_bits)) {   // decode_bch's length check
+        if (lane == 0) a.result[k] = -kEINVAL;
+        return;
+    }
+    const uint32_t nbits = 8u * a.len + (uint32_t)b.ecc_bits;
+    uint8_t *d = a.ecc_only ? nullptr : a.wdata + k * a.dstride, *e = a.ecc + k * a.estride;
+    // syndromes S_1 .. S_2t
+    if (a.syn) {
+        const uint32_t *sin = a.syn + k * a.sstride;
+        uint32_t bad = 0;
+        for (int j = 1 + lane; j <= 2 * T; j += 64) {
+            const uint32_t v = sin[j - 1];
+            bad |= v > n;
+            S[j] = (uint16_t)v;
+        }
+        if (__ballot(bad != 0)) {
+            if (lane == 0) a.result[k] = -kEINVAL;
+            return;
+        }
+    } else {
+        uint64_t w[NWL];
+        if (a.ecc_only) {
+#pragma unroll
+            for (int j = 0; j < NWL; ++j) w[j] = 0;
+        } else {
+            wave_remainder<NWL>(b, a.data + k * a.dstride, a.len, w);
+        }
+        uint64_t any = 0;
+#pragma unroll
+        for (int j = 0; j < NWL; ++j) {
+            const int wi = lane * NWL + j;
+            for (int bb = 0; bb < 8; ++bb) {               // XOR the received ECC (big-endian words)
+                const int i = 8 * wi + bb;
+                if (i < b.ecc_bytes) w[j] ^= (uint64_t)e[i] << (56 - 8 * bb);
+            }
+            const int hi = b.ecc_bits - 64 * wi;           // significant bits of word wi
+            w[j] &= hi >= 64 ? ~0ull : hi <= 0 ? 0ull : ~0ull << (64 - hi);
+            any |= w[j];
+        }
+        if (!__ballot(any != 0)) {
+            if (lane == 0) a.result[k] = 0;
+            return;
+        }
+        // odd S_j from the set bits (powers p) of the remainder, lane-parallel over j
+        for (int j0 = 1; j0 < 2 * T; j0 += 128) {
+            const int j = j0 + 2 * lane;
+            uint32_t acc = 0;
+#pragma unroll
+            for (int jj = 0; jj < NWL; ++jj)
+                for (int ls = 0; ls < 64; ++ls) {
+                    uint64_t x = readlane64(w[jj], ls);
+                    const int wi = ls * NWL + jj;
+                    while (x) {
+                        const int lz = __clzll(x);
+                        x &= ~(0x8000000000000000ull >> lz);
+                        const uint32_t pw = (uint32_t)(b.ecc_bits - 1 - (64 * wi + lz));
+                        if (j < 2 * T) acc ^= f.ex[mod_n((uint32_t)j * pw, m, n)];
+                    }
+                }
+            if (j < 2 * T) S[j] = (uint16_t)acc;
+        }
+        __syncthreads();
+        // even S_(2^k o) = S_o^(2^k): one lookup each
+        for (int j = 2 + 2 * lane; j <= 2 * T; j += 128) {
+            int o = j, sh = 0;
+            while (!(o & 1)) { o >>= 1; ++sh; }
+            const uint32_t so = S[o];
+            S[j] = so ? (uint16_t)f.ex[mod_n((uint32_t)f.lg[so] << sh, m, n)] : (uint16_t)0;
+        }
+    }
+    __syncthreads();
+    // Berlekamp-Massey (as locate_big): C = 1, B = x
+    for (size_t j = lane; j < W; j += 64) {
+        C[j] = j == 0;
+        B[j] = j == 1;
+    }
+    __syncthreads();
+    int L = 0;
+    uint32_t bd = 1;
+    for (int rr = 1; rr < 2 * T; rr += 2) {
+        uint32_t part = 0;
+        const int top = L < rr - 1 ? L : rr - 1;
+        for (int i = 1 + lane; i <= top; i += 64) part ^= f.mul(C[i], S[rr - i]);
+        const uint32_t dd = S[rr] ^ wave_xor(part);
+        const int ch = (int)(W / 64);
+        if (dd) {
+            const bool grow = 2 * L <= rr - 1;
+            const uint32_t q = f.div(dd, bd);
+            for (int c = ch - 1; c >= 0; --c) {            // top-down: [j-2] still holds the old values
+                const int j = 64 * c + lane;
+                const uint32_t cj = C[j], bj = B[j], c2 = j >= 2 ? C[j - 2] : 0u, b2 = j >= 2 ? B[j - 2] : 0u;
+                __syncthreads();
+                C[j] = (uint16_t)(cj ^ f.mul(q, bj));
+                B[j] = (uint16_t)(j >= 2 ? (grow ? c2 : b2) : 0u);
+                __syncthreads();
+            }
+            if (grow) {
+                L = rr - L;
+                bd = dd;
+            }
+        } else {
+            for (int c = ch - 1; c >= 0; --c) {
+                const int j = 64 * c + lane;
+                const uint32_t b2 = j >= 2 ? B[j - 2] : 0u;
+                __syncthreads();
+                B[j] = (uint16_t)b2;
+                __syncthreads();
+            }
+        }
+    }
+    int res;
+    if (L > T || (L > 0 && !C[L])) {
+        res = -kEBADMSG;
+    } else if (L == 0) {
+        res = 0;
+    } else {
+        int nr;
+        if (L <= 4) {
+            if (L == 1) {
+                if (lane == 0) P[0] = f.lg[C[1]];
+                nr = 1;
+            } else {
+                uint32_t X[4];
+                nr = small_roots(f, m, L, C[1], C[2], C[3], L >= 4 ? C[4] : 0u, X);
+                if (lane == 0)
+                    for (int i = 0; i < nr && i < 4; ++i) P[i] = f.lg[X[i]];
+            }
+        } else {
+            for (size_t j = lane; j <= (size_t)L; j += 64) lgC[j] = C[j] ? (int32_t)f.lg[C[j]] : -1;
+            __syncthreads();
+            nr = 0;
+            for (uint32_t p0 = 0; p0 < nbits && nr < L; p0 += 64) {
+                const uint32_t pp = p0 + lane;
+                uint32_t v = 0;
+                for (int j = 0; j <= L; ++j) {
+                    const int lc = lgC[j];
+                    if (lc >= 0) v ^= f.ex[mod_n((uint32_t)lc + mod_n((uint32_t)(L - j) * pp, m, n), m, n)];
+                }
+                const uint64_t hit = __ballot(pp < nbits && v == 0);
+                if (hit) {
+                    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(hit >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)hit, 0u));
+                    if ((hit >> lane) & 1 && nr + (int)below < T) P[nr + below] = pp;
+                    nr += __popcll(hit);
+                }
+            }
+        }
+        __syncthreads();
+        res = L;
+        if (nr != L) res = -kEBADMSG;
+        else {
+            uint32_t bad = 0;
+            for (int i = lane; i < L; i += 64) bad |= P[i] >= nbits;
+            if (__ballot(bad != 0)) res = -kEBADMSG;
+        }
+        if (res > 0) {
+            // error bit e = nbits-1-P, reported as (e & ~7) | (7 - e & 7); rank-sort ascending
+            for (int i = lane; i < L; i += 64) {
+                const uint32_t ei = nbits - 1 - P[i], el = (ei & ~7u) | (7u - (ei & 7u));
+                int rank = 0;
+                for (int q2 = 0; q2 < L; ++q2) {
+                    const uint32_t eq = nbits - 1 - P[q2], lq = (eq & ~7u) | (7u - (eq & 7u));
+                    rank += lq < el;
+                }
+                E[rank] = el;
+            }
+            __syncthreads();
+            if (a.errloc)
+                for (int i = lane; i < L; i += 64) a.errloc[k * a.lstride + i] = E[i];
+            if (!a.ecc_only && !a.syn && lane == 0)
+                for (int i = 0; i < L; ++i) {                  // serial: two errors may share a byte
+                    const uint32_t el = E[i];
+                    if (el < 8u * a.len) d[el >> 3] ^= (uint8_t)(1u << (el & 7));
+                    else e[(el >> 3) - a.len] ^= (uint8_t)(1u << (el & 7));
+                }
+        }
+    }
+    if (lane == 0) a.result[k] = res;
+}
+
 hipError_t launch_encode(const DevBch &b, BchArgs a, hipStream_t s) {
+    if (b.nwl) {
+        const unsigned g = (unsigned)a.ncw;
+        if (b.nwl == 1) hipLaunchKernelGGL(k_bch_encode_wave<1>, dim3(g), dim3(64), 0, s, b, a);
+        else if (b.nwl == 2) hipLaunchKernelGGL(k_bch_encode_wave<2>, dim3(g), dim3(64), 0, s, b, a);
+        else if (b.nwl == 4) hipLaunchKernelGGL(k_bch_encode_wave<4>, dim3(g), dim3(64), 0, s, b, a);
+        else hipLaunchKernelGGL(k_bch_encode_wave<8>, dim3(g), dim3(64), 0, s, b, a);
+        return hipGetLastError();
+    }
     const unsigned grid = (unsigned)((a.ncw + kThreads - 1) / kThreads);
     a.staged = want_staging(b, false, a);
     const size_t sh = lds_bytes(b, false, a);
@@ -691,6 +971,15 @@ hipError_t launch_encode(const DevBch &b, BchArgs a, hipStream_t s) {
 }
 
 hipError_t launch_decode(const DevBch &b, BchArgs a, hipStream_t s) {
+    if (b.nwl) {
+        const unsigned g = (unsigned)a.ncw;
+        const size_t sh = wave_lds_bytes(b.t);
+        if (b.nwl == 1) hipLaunchKernelGGL(k_bch_decode_wave<1>, dim3(g), dim3(64), sh, s, b, a);
+        else if (b.nwl == 2) hipLaunchKernelGGL(k_bch_decode_wave<2>, dim3(g), dim3(64), sh, s, b, a);
+        else if (b.nwl == 4) hipLaunchKernelGGL(k_bch_decode_wave<4>, dim3(g), dim3(64), sh, s, b, a);
+        else hipLaunchKernelGGL(k_bch_decode_wave<8>, dim3(g), dim3(64), sh, s, b, a);
+        return hipGetLastError();
+    }
     const unsigned grid = (unsigned)((a.ncw + kThreads - 1) / kThreads);
     a.staged = a.ecc_only ? 0 : want_staging(b, true, a);
     const size_t sh = lds_bytes(b, true, a);
@@ -797,7 +1086,14 @@ struct HostBch {
         return true;
     }
 
+    // the lane path: t <= 64 and ecc_bits <= 1024; the wave path above
+    bool wave() const { return t > (unsigned)kBigT || ecc_bits > 64u * kMaxNW; }
+    unsigned nwl() const {
+        const unsigned w = (ecc_bits + 63) / 64;             // 64-bit words
+        return !wave() ? 0 : w <= 64 ? 1 : w <= 128 ? 2 : w <= 256 ? 4 : 8;
+    }
     unsigned words() const {
+        if (wave()) return 64 * nwl();
         return ecc_bits <= 64 ? 1 : ecc_bits <= 128 ? 2 : ecc_bits <= 256 ? 4 : ecc_bits <= 512 ? 8 : 16;
     }
     // step[v] = (v x^(E+8 nw 64-8) mod g) left-justified over nw words (w[0] most significant):
@@ -857,10 +1153,6 @@ int create_impl(ezbch_codec **out, unsigned m, unsigned t, unsigned poly, int de
         g_err = "BCH<N,K,T>: K does not match the codec init_bch builds (N - ecc_bits)";
         return -EINVAL;
     }
-    if (t > (unsigned)kBigT || h.ecc_bits > 64u * kMaxNW) {
-        g_err = "BCH device path supports t <= 64 and ecc_bits <= 1024";
-        return -ENOTSUP;
-    }
     int ndev = 0;
     hipError_t e = hipGetDeviceCount(&ndev);
     if (e != hipSuccess || ndev == 0 || device < 0 || device >= ndev) {
@@ -892,7 +1184,8 @@ int create_impl(ezbch_codec **out, unsigned m, unsigned t, unsigned poly, int de
     d.ecc_bytes = (int)c->h.ecc_bytes;
     d.lds_tabs = m <= 12;
     d.nw = (int)c->h.words();
-    for (int i = 0; i < kMaxNW; ++i) {
+    d.nwl = (int)c->h.nwl();
+    for (int i = 0; i < kMaxNW && !d.nwl; ++i) {
         const int hi = (int)c->h.ecc_bits - 64 * i;             // significant bits in word i
         d.emask[i] = hi >= 64 ? ~0ull : hi <= 0 ? 0ull : ~0ull << (64 - hi);
     }

@@ -13,12 +13,12 @@
  * applied independently to every codeword of a batch.  Conventions follow ezrs.h: compute entry
  * points take DEVICE pointers and a hipStream_t passed as void*, are asynchronous and never
  * allocate; the *_host forms take host pointers and block.  Every function returns 0 or a negative
- * errno (-EINVAL bad arguments / parameters init_bch rejects, -ENOTSUP a valid codec outside the
- * device path's limits, -ENODEV no usable HIP device, -ENOMEM, -EIO a HIP error).
+ * errno (-EINVAL bad arguments / parameters init_bch rejects, -ENODEV no usable HIP device, -ENOMEM, -EIO a HIP error).
  *
  * Bit conventions (bch_base:119-123): data bits enter MSB first; the ECC is the remainder
  * left-justified and big-endian in ecc_bytes bytes; an error location e addresses data[e/8] bit
- * (e%8) for e < 8*len and ECC byte e/8-len bit (e%8) beyond.  Device limit: t <= 64 (ecc_bits <= 1024).
+ * (e%8) for e < 8*len and ECC byte e/8-len bit (e%8) beyond.  Every init_bch-valid codec runs on the
+ * device: t <= 64 and ecc_bits <= 1024 one lane per codeword, larger ones one wavefront per codeword.
  */
 #ifndef EZBCH_H
 #define EZBCH_H

@@ -34,7 +34,11 @@ CODECS = [(5, 2), (8, 2), (8, 8), (10, 4), (11, 5), (12, 5), (13, 4), (15, 4), (
           # beyond one 64-bit remainder word and t > 8 (general BCH)
           (13, 8), (10, 9), (14, 12), (15, 16), (12, 16), (6, 10), (9, 13), (16 - 1, 9),
           # t > 16 / ECC > 256 bits: the run-time-t kernel (k_bch_decode_big), 1..16 remainder words
-          (7, 17), (8, 17), (10, 20), (9, 30), (12, 30), (15, 40), (13, 64)]
+          (7, 17), (8, 17), (10, 20), (9, 30), (12, 30), (15, 40), (13, 64),
+          # t > 64 or ECC > 1024 bits: one wavefront per codeword (k_bch_*_wave), every
+          # init_bch-valid codec
+          (10, 65), (12, 90), (13, 100), (15, 200), (11, 120)]
+BIG = {(10, 65), (12, 90), (13, 100), (15, 200), (11, 120)}
 
 
 @pytest.mark.parametrize("m,t", CODECS, ids=[f"m{m}t{t}" for m, t in CODECS])
@@ -44,7 +48,7 @@ def test_device_matches_oracle(torch, m, t):
     assert (c.n, c.ecc_bits, c.ecc_bytes) == (oc.n, oc.ecc_bits, oc.ecc_bytes)
     rng = np.random.default_rng(1000 * m + t)
     for L in sorted({min(oc.max_len, 300), max(1, oc.max_len // 3), 1}):
-        ncw = 2500
+        ncw = 300 if (m, t) in BIG else 2500
         eb = oc.ecc_bytes
         rows = rng.integers(0, 256, (ncw, L + eb), dtype=np.uint8)
         ref = rows.copy()
@@ -167,14 +171,14 @@ def test_c5_full_size_round_trip(torch):
     assert torch.equal(d, rows)
 
 
-@pytest.mark.parametrize("m,t", [(10, 4), (13, 8), (15, 16), (13, 40)])
+@pytest.mark.parametrize("m,t", [(10, 4), (13, 8), (15, 16), (13, 40), (13, 100)])
 def test_decode_from_ecc_difference(torch, m, t):
     """decode_bch's recv XOR calc form (bch_base:96-111; ezbch_decode_ecc): the locations found
     from the ECC difference alone equal those of a full decode of the same corrupted codeword."""
     import ezrs
     oc, c = O.BCH(m, t), ezrs.BCH(m, t)
     rng = np.random.default_rng(7 * m + t)
-    L, ncw, eb = min(oc.max_len, 200), 3000, oc.ecc_bytes
+    L, ncw, eb = min(oc.max_len, 200), 3000 if t <= 64 else 400, oc.ecc_bytes
     ref = rng.integers(0, 256, (ncw, L + eb), dtype=np.uint8)
     oc.encode_batch(ref, L)
     bad = ref.copy()
@@ -196,7 +200,7 @@ def test_decode_from_ecc_difference(torch, m, t):
     np.testing.assert_array_equal(d.cpu().numpy(), diff)        # nothing corrected
 
 
-@pytest.mark.parametrize("m,t", [(10, 4), (13, 8), (15, 16), (10, 20), (13, 40)])
+@pytest.mark.parametrize("m,t", [(10, 4), (13, 8), (15, 16), (10, 20), (13, 40), (12, 90)])
 def test_decode_from_syndromes(torch, m, t):
     """decode_bch's syndrome form (bch_base:112-114; ezbch_decode_syn): syndromes of corrupted
     codewords give the same locations as a full decode, and arbitrary syndrome vectors (not those
@@ -205,7 +209,7 @@ def test_decode_from_syndromes(torch, m, t):
     oc, c = O.BCH(m, t), ezrs.BCH(m, t)
     rng = np.random.default_rng(31 * m + t)
     L, eb = min(oc.max_len, 150), oc.ecc_bytes
-    ncw = 1200
+    ncw = 1200 if t <= 64 else 300
     ref = rng.integers(0, 256, (ncw, L + eb), dtype=np.uint8)
     oc.encode_batch(ref, L)
     bad = ref.copy()

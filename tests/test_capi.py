@@ -72,8 +72,6 @@ def test_bch_invalid_codecs_rejected_before_device():
     assert L.ezbch_create(C.byref(h), 4, 1, 0, 0) == -errno.EINVAL          # m < 5
     assert L.ezbch_create(C.byref(h), 5, 7, 0, 0) == -errno.EINVAL          # m*t >= n
     assert L.ezbch_create(C.byref(h), 8, 2, 0x101, 0) == -errno.EINVAL      # not primitive
-    assert L.ezbch_create(C.byref(h), 10, 65, 0, 0) == -errno.ENOTSUP       # valid, t > 64
-    assert L.ezbch_create(C.byref(h), 15, 100, 0, 0) == -errno.ENOTSUP      # valid, t > 64
     assert L.ezbch_create_nkt(C.byref(h), 255, 240, 2, 0) == -errno.EINVAL  # BCH<255,240,2> mismatch
     assert L.ezbch_create_nkt(C.byref(h), 254, 239, 2, 0) == -errno.EINVAL
     assert not h.value
@@ -87,5 +85,7 @@ def test_bch_no_device_reports_enodev():
     L = ezrs.lib()
     h = C.c_void_p()
     assert L.ezbch_create_nkt(C.byref(h), 1023, 983, 4, 0) == -errno.ENODEV
+    assert L.ezbch_create(C.byref(h), 10, 65, 0, 0) == -errno.ENODEV        # valid, t > 64: wave path
+    assert L.ezbch_create(C.byref(h), 15, 200, 0, 0) == -errno.ENODEV
     with pytest.raises(ezrs.EzrsError):
         ezrs.BCH(8, 2)
