@@ -116,15 +116,22 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
 #pragma unroll
     for (int i = 0; i <= 32; ++i) b[i] = i == 0 ? 0u : L.I[lam[i]];
 
-    // Berlekamp-Massey (1507-1546).  At step r, lambda and B have degree <= r - 1, so blocks of 4
-    // coefficients starting above r hold zeros and are skipped.
+    // Berlekamp-Massey (1507-1546).  Before step r, deg lambda <= el and deg B <= r - 1 - el +
+    // no_eras (the reference's length rule keeps both; checked exhaustively against a model), so
+    // the discrepancy needs coefficients i <= min(r - 1, el) and the update i <= max(el, r - el +
+    // no_eras): coefficient blocks of 4 above those per-lane bounds hold zeros and are skipped
+    // (whole blocks when every lane of the wave is past them).  l[i] = log lambda_i stays the zero
+    // class above el.
+#pragma unroll
+    for (int i = 0; i <= 32; ++i) l[i] = i == 0 ? 0u : kZ;
     unsigned el = no_eras;
     for (unsigned r = no_eras + 1; r <= NR; ++r) {
         const int sb = 32 - (int)r;           // row of S_{r-1}; S_{r-1-i} at row sb + i
+        const unsigned dmax = min(r - 1, el), umax = max(el, r + no_eras - el);
         unsigned discr = 0;
 #pragma unroll
         for (int i0 = 0; i0 <= 32; i0 += 4) {
-            if ((unsigned)i0 <= r) {
+            if ((unsigned)i0 <= dmax) {
 #pragma unroll
                 for (int i = i0; i < i0 + 4 && i <= 32; ++i) {
                     l[i] = i == 0 ? 0u : L.I[lam[i]];
@@ -137,7 +144,7 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
         const unsigned ndl = 255u - dl;
 #pragma unroll
         for (int i0 = 32; i0 >= 0; i0 -= 4) {
-            if ((unsigned)i0 <= r) {
+            if ((unsigned)i0 <= umax) {
 #pragma unroll
                 for (int i = i0 + 3; i >= i0; --i) {
                     if (i > 32) continue;
