@@ -23,6 +23,8 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libezrs_hip.so")
+# timing experiments only: a variant build of the same library (tools/build_variant.sh)
+LIB_PATH = os.environ.get("EZRS_LIB_VARIANT") or LIB_PATH
 HEADER = os.path.join(os.path.dirname(HERE), "include", "ezrs.h")
 BCH_HEADER = os.path.join(os.path.dirname(HERE), "include", "ezbch.h")
 
