@@ -26,7 +26,9 @@ CALLS = {
 
 
 def kernel_call(name):
-    if "k_py_syndromes" in name or "k_pg_syndromes" in name or "k_pt_lin" in name:
+    if "k_pt_lin<" in name:                      # k_pt_lin<codec, ENC, SH>
+        return "ezrs_encode" if name.split("k_pt_lin<")[1].split(",")[1].strip() == "true" else "ezrs_decode"
+    if "k_py_syndromes" in name or "k_pg_syndromes" in name:
         return "ezrs_encode" if "true>" in name else "ezrs_decode"
     for call, keys in (("ezrs_encode", ("k_ps_parity", "k_wide_finish<true>")),
                        ("ezrs_decode", ("k_decode_errors", "k_wide_finish<false>", "k_wide_errors")),
