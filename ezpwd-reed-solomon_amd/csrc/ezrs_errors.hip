@@ -220,7 +220,13 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
             }
         }
         const unsigned top = (deg < NR - 1 ? deg : NR - 1) & ~1u;
-        // Forney, roots in reverse order, corrections applied as found (1610-1690)
+        // Forney, roots in reverse order (1610-1690).  The reference applies each correction as it
+        // is found and keeps the ones before a failure; here they are recorded (position, value) in
+        // the syndrome rows -- dead once Omega is formed -- and applied afterwards with the row
+        // bytes loaded eight at a time, so the byte read-modify-writes of a codeword overlap their
+        // global-memory latency instead of paying it once per correction.  The dual basis (CCSDS)
+        // needs each received byte to form its correction and keeps the in-order path.
+        unsigned nrec = 0;
         for (int j = count - 1; j >= 0; --j) {
             const unsigned rj = W.root[j * 64 + lane];
             unsigned num1 = 0, den = 0, e = 0;     // e = i * rj (mod 255)
@@ -241,6 +247,11 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
                 if (loc < pad) { count = -1; break; }
                 const unsigned n2 = (unsigned)(((int)rj * ((int)FCR - 1)) % 255 + 255) % 255u;
                 const unsigned cor = L.A[(L.I[num1] + n2 + 255u - L.I[den]) % 255u];
+                if (!c.dual) {
+                    S(nrec++) = (uint16_t)(loc << 8 | cor);
+                    if (corr_out) corr_out[j] = (uint8_t)cor;
+                    continue;
+                }
                 unsigned cv = cor, delta = cor;
                 uint8_t *at;
                 if (loc < 255u - NR) {
@@ -260,6 +271,22 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
                 *at = (uint8_t)(*at ^ delta);
                 if (corr_out) corr_out[j] = (uint8_t)cv;
             }
+        }
+        for (unsigned g0 = 0; g0 < nrec; g0 += 8) {
+            uint8_t *at[8];
+            unsigned v[8], dlt[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                if (g0 + t < nrec) {
+                    const unsigned rec = S(g0 + t), loc = rec >> 8;
+                    dlt[t] = rec & 255u;
+                    at[t] = loc < 255u - NR ? data + (loc - pad) : parity + (loc - (255u - NR));
+                    v[t] = *at[t];
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+                if (g0 + t < nrec) *at[t] = (uint8_t)(v[t] ^ dlt[t]);
         }
     }
     if (pos_out && count > 0)
