@@ -287,7 +287,7 @@ hipError_t dispatch_encode(const ezrs_codec *c, const EncodeArgs &a, void *ws, h
     return c->bs_id >= 0 ? launch_bs_encode(c->bs_id, c->dev, a, ws, st) : launch_encode_generic(c->dev, a, st);
 }
 
-// syn_ws: [ncw][32] bytes (bit-sliced path only).
+// syn_ws: the sliced paths' syndrome workspace (ws_bytes_for).
 hipError_t dispatch_decode(const ezrs_codec *c, const DecodeArgs &a, uint8_t *syn_ws,
                            hipStream_t st) {
     const unsigned w = c->dev.mm <= 8 ? 1 : 2;
@@ -295,7 +295,7 @@ hipError_t dispatch_decode(const ezrs_codec *c, const DecodeArgs &a, uint8_t *sy
                             a.parity_stride == a.data_stride;
     if (c->ps_id >= 0 && ps_can_decode(c->dev, a)) {
         hipError_t e = launch_ps_syndromes(c->ps_id, c->dev, a, syn_ws, st);
-        if (e == hipSuccess) e = launch_decode_flagged(c->dev, a, syn_ws, st);
+        if (e == hipSuccess) e = launch_decode_flagged(c->dev, a, syn_ws, SynLayout::Tiled, st);
         return e;
     }
     if (a.sh.rows) return launch_decode_generic(c->dev, a, st);     // shard rows: per-codeword kernels
@@ -305,7 +305,7 @@ hipError_t dispatch_decode(const ezrs_codec *c, const DecodeArgs &a, uint8_t *sy
         // Bit-sliced syndromes for the whole batch; the reference algorithm only for the codewords
         // that are not valid as received (or carry erasures to validate).
         hipError_t e = launch_bs_syndromes(c->bs_id, c->dev, a, syn_ws, st);
-        if (e == hipSuccess) e = launch_decode_flagged(c->dev, a, syn_ws, st);
+        if (e == hipSuccess) e = launch_decode_flagged(c->dev, a, syn_ws, SynLayout::Rows, st);
         return e;
     }
     return launch_decode_generic(c->dev, a, st);

@@ -30,6 +30,7 @@ namespace ezrs {
 namespace {
 
 constexpr int32_t kSentinel = INT32_MIN;
+
 constexpr int kSpan = 256;              // result slots screened per wavefront
 constexpr int kWaves = 16;              // wavefronts per workgroup (one workgroup per CU)
 constexpr unsigned kZ = 1024;           // log(0); every value >= 510 is in the zero class
@@ -58,11 +59,21 @@ struct Lds {
     WaveLds w[kWaves];
 };
 
+// Table reads of the decode; gp: the antilog of a sum of two logs (either may be in the zero class).
+// Measured and dropped (C3 decode 0.767 ms): 8-byte antilog reads banked mod 64 (60+ VGPRs of
+// spills), a per-bank replicated antilog table (3 more VALU per read: 0.871 ms), an antilog table
+// extended over every sum instead of pidx (fewer VALU, more bank conflicts: 0.777 ms), and B
+// updates skipped in wave-uniform branches (170+ VGPRs of spills).
+__device__ __forceinline__ unsigned ga(const Lds &L, unsigned x) { return L.A[x]; }
+__device__ __forceinline__ unsigned gi(const Lds &L, unsigned x) { return L.I[x]; }
+__device__ __forceinline__ unsigned gp(const Lds &L, unsigned x) { return L.A[pidx(x)]; }
+
 __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, const Lds &L, WaveLds &W,
                                                           const unsigned lane, uint8_t *data, unsigned len,
                                                           uint8_t *parity, const uint32_t *eras,
                                                           unsigned no_eras, uint32_t *pos_out,
-                                                          uint8_t *corr_out, const uint8_t *syn_in) {
+                                                          uint8_t *corr_out, const uint8_t *syn_in,
+                                                          unsigned syn_step) {
     const unsigned NR = c.nroots, LOAD = c.load, FCR = c.fcr, PRM = c.prim;
     if (len == 0 || len > LOAD) return -1;                                    // 1375-1377
     if (no_eras > NR) return -1;                                              // 1380-1382
@@ -71,20 +82,15 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
     const unsigned pad = LOAD - len;
     auto S = [&](int k) -> uint16_t & { return W.srev[k * 64 + lane]; };
 
-    // syndromes (polynomial form from the syndrome kernel) -> logs, stored reversed (1416-1434)
+    // syndromes (polynomial form from the syndrome kernel; syndrome i at syn_in[i * syn_step]) ->
+    // logs, stored reversed (1416-1434)
     unsigned syn_error = 0;
     {
-        uint4 w0 = make_uint4(0, 0, 0, 0), w1 = w0;
-        if (syn_in) {
-            __builtin_memcpy(&w0, syn_in, 16);
-            __builtin_memcpy(&w1, syn_in + 16, 16);
-        }
-        const unsigned w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
 #pragma unroll
         for (int i = 0; i < 32; ++i) {
-            const unsigned v = i < (int)NR ? (w[i >> 2] >> (8 * (i & 3))) & 255u : 0u;
+            const unsigned v = syn_in && i < (int)NR ? syn_in[i * syn_step] : 0u;
             syn_error |= v;
-            S(31 - i) = L.I[v];
+            S(31 - i) = gi(L, v);
         }
 #pragma unroll
         for (int k = 32; k < kSrows; ++k) S(k) = kZ;
@@ -96,7 +102,7 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
 #pragma unroll
     for (int i = 0; i <= 32; ++i) lam[i] = i == 0;
     if (no_eras > 0) {
-        lam[1] = L.A[(PRM * (c.nn - 1 - (eras[0] + pad))) % 255u];
+        lam[1] = ga(L, (PRM * (c.nn - 1 - (eras[0] + pad))) % 255u);
         for (unsigned e = 1; e < no_eras; ++e) {
             const unsigned u = (PRM * (c.nn - 1 - (eras[e] + pad))) % 255u;
             // lam[j] ^= lam[j-1] * alpha^u for j = e+1 .. 1 (lam[j-1] == 0 for j - 1 > e)
@@ -106,7 +112,7 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
 #pragma unroll
                     for (int j = j0 + 3; j >= j0; --j) {
                         if (j < 1 || j > 32) continue;
-                        lam[j] ^= L.A[pidx(u + L.I[lam[j - 1]])];
+                        lam[j] ^= gp(L, (u + gi(L, lam[j - 1])));
                     }
                 }
             }
@@ -114,7 +120,7 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
     }
     unsigned b[33], l[33];
 #pragma unroll
-    for (int i = 0; i <= 32; ++i) b[i] = i == 0 ? 0u : L.I[lam[i]];
+    for (int i = 0; i <= 32; ++i) b[i] = i == 0 ? 0u : gi(L, lam[i]);
 
     // Berlekamp-Massey (1507-1546).  Before step r, deg lambda <= el and deg B <= r - 1 - el +
     // no_eras (the reference's length rule keeps both; checked exhaustively against a model), so
@@ -134,12 +140,12 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
             if ((unsigned)i0 <= dmax) {
 #pragma unroll
                 for (int i = i0; i < i0 + 4 && i <= 32; ++i) {
-                    l[i] = i == 0 ? 0u : L.I[lam[i]];
-                    if (i < 32) discr ^= L.A[pidx(l[i] + S(sb + i))];
+                    l[i] = i == 0 ? 0u : gi(L, lam[i]);
+                    if (i < 32) discr ^= gp(L, (l[i] + S(sb + i)));
                 }
             }
         }
-        const unsigned dl = L.I[discr];
+        const unsigned dl = gi(L, discr);
         const bool upd = dl < 510u && 2 * el <= r + no_eras - 1;
         const unsigned ndl = 255u - dl;
 #pragma unroll
@@ -149,7 +155,7 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
                 for (int i = i0 + 3; i >= i0; --i) {
                     if (i > 32) continue;
                     const unsigned bp = i > 0 ? b[i - 1] : kZ;
-                    if (i > 0) lam[i] ^= L.A[pidx(dl + bp)];
+                    if (i > 0) lam[i] ^= gp(L, (dl + bp));
                     const unsigned d = l[i] + ndl;
                     const unsigned nb = min(min(d, d - 255u), kZ);
                     b[i] = upd ? nb : bp;
@@ -163,7 +169,7 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
     unsigned deg = 0;
 #pragma unroll
     for (int i = 0; i <= 32; ++i) {
-        l[i] = i == 0 ? 0u : L.I[lam[i]];
+        l[i] = i == 0 ? 0u : gi(L, lam[i]);
         if (i > 0 && lam[i] != 0) deg = i;
     }
 
@@ -214,8 +220,8 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
                 for (int i = i0; i < i0 + 4; ++i) {
                     unsigned t = 0;
 #pragma unroll
-                    for (int j = 0; j <= i; ++j) t ^= L.A[pidx(S(31 - (i - j)) + l[j])];
-                    om[i] = L.I[t];
+                    for (int j = 0; j <= i; ++j) t ^= gp(L, (S(31 - (i - j)) + l[j]));
+                    om[i] = gi(L, t);
                 }
             }
         }
@@ -224,8 +230,9 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
         // is found and keeps the ones before a failure; here they are recorded (position, value) in
         // the syndrome rows -- dead once Omega is formed -- and applied afterwards with the row
         // bytes loaded eight at a time, so the byte read-modify-writes of a codeword overlap their
-        // global-memory latency instead of paying it once per correction.  The dual basis (CCSDS)
-        // needs each received byte to form its correction and keeps the in-order path.
+        // global-memory latency instead of paying it once per correction (atomic XORs of the
+        // dwords instead: 0.99 against 0.78 ms per C3 decode).  The dual basis (CCSDS) needs each
+        // received byte to form its correction and keeps the in-order path.
         unsigned nrec = 0;
         for (int j = count - 1; j >= 0; --j) {
             const unsigned rj = W.root[j * 64 + lane];
@@ -235,8 +242,8 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
                 if ((unsigned)i0 <= deg_omega) {
 #pragma unroll
                     for (int i = i0; i < i0 + 4; ++i) {
-                        if ((unsigned)i <= deg_omega) num1 ^= L.A[pidx(om[i] + e)];
-                        if ((i & 1) == 0 && (unsigned)i <= top) den ^= L.A[pidx(l[i + 1] + e)];
+                        if ((unsigned)i <= deg_omega) num1 ^= gp(L, (om[i] + e));
+                        if ((i & 1) == 0 && (unsigned)i <= top) den ^= gp(L, (l[i + 1] + e));
                         e = addmod(e, rj);
                     }
                 }
@@ -246,7 +253,7 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
                 const unsigned loc = (rj * c.iprim + 254u) % 255u;
                 if (loc < pad) { count = -1; break; }
                 const unsigned n2 = (unsigned)(((int)rj * ((int)FCR - 1)) % 255 + 255) % 255u;
-                const unsigned cor = L.A[(L.I[num1] + n2 + 255u - L.I[den]) % 255u];
+                const unsigned cor = ga(L, (gi(L, num1) + n2 + 255u - gi(L, den)) % 255u);
                 if (!c.dual) {
                     S(nrec++) = (uint16_t)(loc << 8 | cor);
                     if (corr_out) corr_out[j] = (uint8_t)cor;
@@ -336,7 +343,8 @@ __device__ __forceinline__ unsigned screen(const DecodeArgs &a, size_t sp, unsig
     return nflag;
 }
 
-__global__ void __launch_bounds__(64 * kWaves) k_decode_errors(DevCodec c, DecodeArgs a, const uint8_t *syn_ws) {
+__global__ void __launch_bounds__(64 * kWaves) k_decode_errors(DevCodec c, DecodeArgs a, const uint8_t *syn_ws,
+                                                              SynLayout layout) {
     __shared__ __attribute__((aligned(16))) Lds L;
     const unsigned lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const size_t nspan = (a.ncw + kSpan - 1) / kSpan, step = (size_t)gridDim.x * kWaves;
@@ -376,8 +384,10 @@ __global__ void __launch_bounds__(64 * kWaves) k_decode_errors(DevCodec c, Decod
                 // a slot that does not hold the sentinel was flagged for its erasures only: its
                 // syndromes are zero and were not written
                 const bool synz = a.result[k] != kSentinel;
+                const bool tiled = layout == SynLayout::Tiled;
+                const uint8_t *syn = tiled ? syn_ws + k / 256 * kSynTile + k % 256 : syn_ws + k * 32;
                 a.result[k] = decode_lane(c, L, W, lane, data, len, parity, eras, ne, pos, corr,
-                                          synz ? nullptr : syn_ws + k * 32);
+                                          synz ? nullptr : syn, tiled ? 256u : 1u);
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // list reads done before the next span
@@ -387,14 +397,14 @@ __global__ void __launch_bounds__(64 * kWaves) k_decode_errors(DevCodec c, Decod
 } // namespace
 
 hipError_t launch_decode_flagged(const DevCodec &c, const DecodeArgs &a, const uint8_t *syn_ws,
-                                 hipStream_t s) {
+                                 SynLayout layout, hipStream_t s) {
     if (a.ncw == 0) return hipSuccess;
     if (c.mm != 8 || c.nroots > 32 || c.masked) return hipErrorInvalidValue;
     const size_t nspan = (a.ncw + kSpan - 1) / kSpan;
     const size_t want = (nspan + kWaves - 1) / kWaves;
     const size_t ncu = c.ncu > 0 ? (size_t)c.ncu : 256;    // attribute query failed: assume 256
     const unsigned grid = (unsigned)(want < ncu ? want : ncu);
-    hipLaunchKernelGGL(k_decode_errors, dim3(grid), dim3(64 * kWaves), 0, s, c, a, syn_ws);
+    hipLaunchKernelGGL(k_decode_errors, dim3(grid), dim3(64 * kWaves), 0, s, c, a, syn_ws, layout);
     return hipGetLastError();
 }
 

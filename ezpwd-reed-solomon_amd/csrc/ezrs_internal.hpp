@@ -104,10 +104,16 @@ __host__ __device__ __forceinline__ void row_ptrs(const A &a, size_t k, P *&data
 // Generic per-codeword kernels (ezrs_generic.hip): every codec, every length.
 hipError_t launch_encode_generic(const DevCodec &c, const EncodeArgs &a, hipStream_t s);
 hipError_t launch_decode_generic(const DevCodec &c, const DecodeArgs &a, hipStream_t s);
-// Error path behind the bit-sliced syndrome kernel: decodes the codewords whose result holds the
-// sentinel, starting from the syndromes in syn_ws ([ncw][32] bytes).
+// Syndrome workspace layouts the error path reads.  Rows: [ncw][32] bytes (bit-sliced kernels).
+// Tiled (plane-sliced kernels): codeword k's syndrome j at (k / 256) * kSynTile + 256 j + k % 256,
+// so the syndrome kernel stores four codewords' syndrome j as one dword and the error path's loads
+// of one syndrome across a wavefront's codewords fall in one or two cache lines.
+constexpr size_t kSynTile = 256 * 32;
+enum class SynLayout { Rows, Tiled };
+// Error path behind the sliced syndrome kernels: decodes the codewords whose result holds the
+// sentinel, starting from the syndromes in syn_ws.
 hipError_t launch_decode_flagged(const DevCodec &c, const DecodeArgs &a, const uint8_t *syn_ws,
-                                 hipStream_t s);
+                                 SynLayout layout, hipStream_t s);
 
 // Bit-sliced GF(2^8) kernels (ezrs_bitslice.hip) for the codecs of gen/ezrs_bs_tables.inc.
 int bitslice_codec_id(const DevCodec &d);   // -1 if the codec has no bit-sliced path

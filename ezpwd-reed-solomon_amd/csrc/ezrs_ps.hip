@@ -68,8 +68,9 @@ struct PsArgs {
     uint32_t ntiles;
     int lo;                     // full-frame position of the rows' first byte (the pad)
     int32_t *result;            // decode
-    uint8_t *ws;                // decode: [ncw][32] flagged syndromes; encode: [NR][ws_pitch]
-    size_t ws_pitch;            // encode: codewords per syndrome row (a multiple of 2048)
+    uint8_t *ws;                // decode: tiled syndromes (kSynTile); encode: [NR][ws_pitch]
+    size_t ws_pitch;            // encode: codewords per syndrome row (a multiple of 2048); decode:
+                                // the launch's first codeword mod 256 (its place in the tiled layout)
     uint32_t srows;             // shard batches (Shards): codewords per shard, 0 = a plain batch
     int stail_lo;               // full-frame position of a shard's last row's first byte
     uint32_t spitch;            // shard pitch in bytes
@@ -433,12 +434,23 @@ __device__ __forceinline__ void wave_tail_lin(uint32_t (&V)[C::NI][8], const PsA
         }
         if (__ballot(fl != 0) != 0) {                        // flagged codewords: their syndromes
             transpose8(Qs);                                  // Qs[jj] byte k: syndrome jj, codeword k
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t row = (fl >> k & 1) ? (cw0 + k) * 32u : kOob;
+            // tiled layout (ezrs_internal.hpp kSynTile): syndrome j of the 256 codewords of a tile in
+            // one 256-byte row, so a lane's four codewords are one dword (unflagged ones included)
+            if (a.ws_pitch == 0) {
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj)
-                    if (C::SYN[W][0][jj] >= 0) store_byte(rws, row + C::SYN[W][0][jj], Qs[jj] >> (8 * k));
+                    if (C::SYN[W][0][jj] >= 0)
+                        store_dword(rws, tile * (uint32_t)kSynTile + 256u * C::SYN[W][0][jj] + 4u * fresh(),
+                                    Qs[jj]);
+            } else {                                         // a launch not starting a tile (shards)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t g = (uint32_t)a.ws_pitch + cw0 + k;
+                    const uint32_t row = (fl >> k & 1) ? (g >> 8) * (uint32_t)kSynTile + (g & 255u) : kOob;
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj)
+                        if (C::SYN[W][0][jj] >= 0) store_byte(rws, row + 256u * C::SYN[W][0][jj], Qs[jj] >> (8 * k));
+                }
             }
         }
     }
@@ -451,7 +463,8 @@ __device__ __forceinline__ void pt_run_lin(const PsArgs &a, uint8_t *lds, int w)
     const pw_rsrc_t rsrc = pw_rsrc(a.base, a.span);
     const uint32_t lbuf = __builtin_amdgcn_readfirstlane(lds_addr(lds));
     const pw_rsrc_t rout = pw_rsrc(reinterpret_cast<const uint8_t *>(a.result), ENC ? 0u : a.ncw * 4u);
-    const pw_rsrc_t rws = pw_rsrc(a.ws, ENC ? (uint32_t)(C::NR * a.ws_pitch) : a.ncw * 32u);
+    const pw_rsrc_t rws = pw_rsrc(a.ws, ENC ? (uint32_t)(C::NR * a.ws_pitch)
+                                            : (uint32_t)((a.ws_pitch + a.ncw + 255) / 256 * kSynTile));
     constexpr bool shards = SH;
     // byte range of tile t: plain batches t * 256 rows of pitch stride; shard batches from its first
     // row's start to the next tile's (the span's end for the last tile)
@@ -691,7 +704,7 @@ static int pt_ablate() {
     return e ? atoi(e) : 0;
 }
 
-// Workspace: decode [ncw][32] flagged syndromes; encode [NR][ws_pitch] syndromes, ws_pitch = ncw
+// Workspace: decode tiled syndromes (kSynTile); encode [NR][ws_pitch] syndromes, ws_pitch = ncw
 // rounded up to 2048 (the parity kernel's block).
 static size_t ps_pitch(size_t ncw) { return (ncw + 2047) / 2048 * 2048; }
 size_t ps_ws_bytes(size_t ncw) { return ps_pitch(ncw) * 32; }
@@ -792,7 +805,8 @@ hipError_t launch_ps_syndromes(int id, const DevCodec &d, const DecodeArgs &a, u
         p.ntiles = (uint32_t)((n + ps::kTile - 1) / ps::kTile);
         p.lo = (int)(d.load - a.len);
         p.result = a.result + k0;
-        p.ws = syn_ws + k0 * 32;
+        p.ws = syn_ws + k0 / 256 * kSynTile;                  // tiled layout, global codeword index
+        p.ws_pitch = k0 % 256;
         p.ablate = pt_ablate();
         const unsigned grid = syn_grid(d, p.ntiles);
         int k = 0;
