@@ -76,6 +76,38 @@ def test_device_matches_oracle(torch, m, t):
         assert (res[np.arange(ncw) % (t + 3) <= t] >= 0).all()
 
 
+@pytest.mark.parametrize("L,pitch", [(95, 0), (96, 0), (97, 0), (99, 0), (101, 0), (122, 0), (127, 0),
+                                     (128, 0), (129, 0), (131, 0), (200, 0), (120, 600), (130, 700)])
+def test_split_remainder_lengths(torch, L, pitch):
+    """1-word codecs (ecc_bits <= 64) take the four-chain remainder from 3 kQ = 96 data bytes on:
+    stream 0 starting before the row (L < 128) or after a head chain (L > 128), every row
+    alignment (odd strides), and rows read in place (a pitch too wide to stage in LDS)."""
+    import ezrs
+    oc, c = O.BCH(12, 5), ezrs.BCH(12, 5)
+    eb, ncw = oc.ecc_bytes, 700
+    w = max(pitch, L + eb)
+    rng = np.random.default_rng(L * 31 + pitch)
+    rows = rng.integers(0, 256, (ncw, w), dtype=np.uint8)
+    ref = rows.copy()
+    sub = ref[:, :L + eb].copy()
+    oc.encode_batch(sub, L, nthreads=8)
+    ref[:, :L + eb] = sub
+    dev = torch.from_numpy(rows).cuda()
+    c.encode(dev, L)
+    np.testing.assert_array_equal(dev.cpu().numpy(), ref, err_msg="encode")
+    bad = ref.copy()
+    sub = bad[:, :L + eb].copy()
+    _flip(sub, 8 * L + oc.ecc_bits, np.arange(ncw) % 8, rng)
+    bad[:, :L + eb] = sub
+    exp = bad.copy()
+    eres = oc.decode_batch(sub, L, nthreads=8)
+    exp[:, :L + eb] = sub
+    d = torch.from_numpy(bad).cuda()
+    res = c.decode(d, L).cpu().numpy()
+    np.testing.assert_array_equal(res, eres, err_msg="result")
+    np.testing.assert_array_equal(d.cpu().numpy(), exp, err_msg="data")
+
+
 def test_separate_ecc_and_too_long(torch):
     import ezrs
     oc, c = O.BCH(10, 4), ezrs.BCH.nkt(1023, 983, 4)
