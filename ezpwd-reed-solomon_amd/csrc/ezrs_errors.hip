@@ -71,14 +71,45 @@ __device__ __forceinline__ unsigned gp(const Lds &L, unsigned x) { return L.A[pi
 __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, const Lds &L, WaveLds &W,
                                                           const unsigned lane, uint8_t *data, unsigned len,
                                                           uint8_t *parity, const uint32_t *eras,
-                                                          unsigned no_eras, uint32_t *pos_out,
+                                                          unsigned no_eras, unsigned eras_cap, uint32_t *pos_out,
                                                           uint8_t *corr_out, const uint8_t *syn_in,
                                                           unsigned syn_step) {
     const unsigned NR = c.nroots, LOAD = c.load, FCR = c.fcr, PRM = c.prim;
     if (len == 0 || len > LOAD) return -1;                                    // 1375-1377
     if (no_eras > NR) return -1;                                              // 1380-1382
-    for (unsigned i = 0; i < no_eras; ++i)
-        if (eras[i] >= len + NR) return -1;                                   // 1383-1387
+    // erasure positions (1383-1387): loaded four at a time where the row allows (all loads issued
+    // before the first use) and kept as bytes in this lane's Chien root column, free until the
+    // search, for the erasure locator
+    if (no_eras > 0) {
+        unsigned bad = 0;
+        uint8_t *ep = W.root + lane;
+        if ((reinterpret_cast<uintptr_t>(eras) & 15) == 0 && ((no_eras + 3) & ~3u) <= eras_cap) {
+            uint4 v[8];
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+                if (4u * c < no_eras) __builtin_memcpy(&v[c], eras + 4 * c, 16);
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                if (4u * c < no_eras) {
+                    const unsigned x[4] = {v[c].x, v[c].y, v[c].z, v[c].w};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        if (4u * c + q < no_eras) {
+                            bad |= x[q] >= len + NR;
+                            ep[(4 * c + q) * 64] = (uint8_t)x[q];
+                        }
+                    }
+                }
+            }
+        } else {
+            for (unsigned i = 0; i < no_eras; ++i) {
+                const unsigned x = eras[i];
+                bad |= x >= len + NR;
+                ep[i * 64] = (uint8_t)x;
+            }
+        }
+        if (bad) return -1;
+    }
     const unsigned pad = LOAD - len;
     auto S = [&](int k) -> uint16_t & { return W.srev[k * 64 + lane]; };
 
@@ -102,9 +133,9 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
 #pragma unroll
     for (int i = 0; i <= 32; ++i) lam[i] = i == 0;
     if (no_eras > 0) {
-        lam[1] = ga(L, (PRM * (c.nn - 1 - (eras[0] + pad))) % 255u);
+        lam[1] = ga(L, (PRM * (c.nn - 1 - (W.root[lane] + pad))) % 255u);
         for (unsigned e = 1; e < no_eras; ++e) {
-            const unsigned u = (PRM * (c.nn - 1 - (eras[e] + pad))) % 255u;
+            const unsigned u = (PRM * (c.nn - 1 - (W.root[e * 64 + lane] + pad))) % 255u;
             // lam[j] ^= lam[j-1] * alpha^u for j = e+1 .. 1 (lam[j-1] == 0 for j - 1 > e)
 #pragma unroll
             for (int j0 = 32; j0 >= 0; j0 -= 4) {
@@ -386,7 +417,8 @@ __global__ void __launch_bounds__(64 * kWaves) k_decode_errors(DevCodec c, Decod
                 const bool synz = a.result[k] != kSentinel;
                 const bool tiled = layout == SynLayout::Tiled;
                 const uint8_t *syn = tiled ? syn_ws + k / 256 * kSynTile + k % 256 : syn_ws + k * 32;
-                a.result[k] = decode_lane(c, L, W, lane, data, len, parity, eras, ne, pos, corr,
+                const unsigned cap = a.eras_stride < 32 ? (unsigned)a.eras_stride : 32u;
+                a.result[k] = decode_lane(c, L, W, lane, data, len, parity, eras, ne, cap, pos, corr,
                                           synz ? nullptr : syn, tiled ? 256u : 1u);
             }
         }

@@ -1,3 +1,6 @@
 set -u
-bash tools/gpu_pmc1.sh r03w_a "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU" --workload c5 || exit 1
-bash tools/gpu_pmc1.sh r03w_b "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_MISC SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" --workload c5 || exit 1
+OUT=gpurun_out/r03y; mkdir -p $OUT
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "bulk or golden or c3 or shards or karn or host or errors or eras" > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
+tail -1 $OUT/pytest.log
+timeout -k 10 120 python tools/c3_decode_time.py || exit 1
+timeout -k 10 120 python tools/c3_decode_time.py || exit 1

@@ -1,6 +1,6 @@
 #!/bin/bash
 # One round-check on the GPU box: all GPU tests, smoke, the bench lines of every config, kernel-trace
-# summaries (C2, C4, C5) and the FETCH_SIZE / WRITE_SIZE PMC passes (one counter group per run).
+# summaries (C2, C3, C4, C5) and the FETCH_SIZE / WRITE_SIZE PMC passes (one counter group per run).
 set -u
 TAG=${1:-round}; OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG; mkdir -p $OUT
 export TMPDIR=/tmp
@@ -27,7 +27,8 @@ B="python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline"
 run prof_c2 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c2 -o run -- $B --steps 5 --warmup 1
 run prof_c4 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c4 -o run -- $B --workload c4 --steps 2 --warmup 1
 run prof_c5 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c5 -o run -- $B --workload c5 --steps 5 --warmup 1
-for w in c2 c4 c5; do
+run prof_c3 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c3 -o run -- $B --workload c3 --steps 5 --warmup 1
+for w in c2 c3 c4 c5; do
   for grp in FETCH_SIZE WRITE_SIZE; do
     run pmc_${w}_$grp 180 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc_$w/$grp -o run -- $B --workload $w --steps 2 --warmup 1
   done
