@@ -390,3 +390,58 @@ def test_shapes_vs_oracle(torch, maker, L, ncw, extra):
     pos = pos.cpu().numpy().view(np.uint32)
     for k in np.nonzero(r > 0)[0]:
         np.testing.assert_array_equal(pos[k, :r[k]], exp_pos[k, :r[k]])
+
+
+@pytest.mark.parametrize("maker", ["RS(255,223)", "RS_CCSDS_CONV(255,239)", "RS(255,247)"])
+def test_erasure_split_vs_oracle(torch, maker):
+    """1..4 erasures (the error path's Chien over lambda / Gamma): erasures on corrupted and on
+    clean positions, repeated erasure positions, and error loads past capacity, against the
+    oracle's result, positions and corrected rows."""
+    import ezrs
+    if maker.startswith("RS_CCSDS_CONV"):
+        c, oc = ezrs.Codec.ccsds(239, dual=False), O.Codec(*O.ccsds_params(239, False))
+    else:
+        k = int(maker[7:-1])
+        c, oc = ezrs.Codec.rs(255, k), O.Codec(*O.rs_params(255, k))
+    assert c.kernel_path == "planeslice"
+    rng = np.random.default_rng(23)
+    ncw, nr = 20000, c.nroots
+    L = c.load - int(rng.integers(0, 40))
+    ref = rng.integers(0, 256, (ncw, L + nr)).astype(np.uint8)
+    oc.encode_batch(ref, L, None, nthreads=8)
+    cw = ref.copy()
+    eras = np.zeros((ncw, nr), np.uint32)
+    neras = np.zeros(ncw, np.uint32)
+    for k in range(ncw):
+        ne = int(rng.integers(1, 5)) if nr >= 4 else int(rng.integers(1, nr + 1))
+        nerr = int(rng.integers(0, (nr - ne) // 2 + 3))          # up to 2 past capacity
+        locs = rng.choice(L + nr, nerr + ne, replace=False)
+        cw[k, locs[:nerr]] ^= rng.integers(1, 256, nerr).astype(np.uint8)
+        kind = k % 4
+        if kind == 0:
+            e = locs[nerr:]                                         # clean positions
+        elif kind == 1:
+            e = locs[:ne] if nerr >= ne else locs[nerr:]            # on corrupted positions
+        elif kind == 2:
+            e = np.concatenate([locs[nerr:], locs[:0]])
+            if ne >= 2:
+                e = e.copy(); e[-1] = e[0]                          # a repeated position
+        else:
+            e = locs[nerr:].copy()
+            cw[k, e[0]] ^= 0x3C                                      # an erased symbol also wrong
+        eras[k, :ne] = e[:ne]
+        neras[k] = ne
+    exp = cw.copy()
+    exp_pos = np.zeros((ncw, nr), np.uint32)
+    exp_r = oc.decode_batch(exp, L, None, eras, neras, exp_pos, nthreads=8)
+    dcw = torch.from_numpy(cw).cuda()
+    pos = torch.zeros((ncw, nr), dtype=torch.int32, device="cuda")
+    r = c.decode(dcw, L, None, eras=torch.from_numpy(eras.view(np.int32)).cuda(),
+                 neras=torch.from_numpy(neras.view(np.int32)).cuda(), positions=pos)
+    r = r.cpu().numpy()
+    np.testing.assert_array_equal(r, exp_r)
+    np.testing.assert_array_equal(dcw.cpu().numpy(), exp)
+    pos = pos.cpu().numpy().view(np.uint32)
+    for k in np.nonzero(r > 0)[0]:
+        np.testing.assert_array_equal(pos[k, :r[k]], exp_pos[k, :r[k]])
+    assert (r == -1).any() and (r > 0).any()
