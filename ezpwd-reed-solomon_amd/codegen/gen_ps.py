@@ -520,7 +520,7 @@ def gen_pt(c: PsCodec):
            "    // syndrome index of quad slot (W, quad, j), -1 = none",
            f"    static constexpr int SYN[{W}][{R.nq}][4] = " + "{" + ", ".join(
                "{" + ", ".join(fmt_list(q) for q in syn[w]) + "}" for w in range(W)) + "};",
-           "    // positions 8B..8B+7 (words X) into group G's state, B a block of quarter 0",
+           "    // positions 8B..8B+7 (words X) into group G's state (B: the absolute 8-position block)",
            "    template <int G, int B> static __device__ void block(uint32_t (&V)[NI][8], const uint32_t (&X)[8]);",
            "    // group G's partials of quarter Q (computed with quarter 0's weights) times alpha^(-16 Q e)",
            "    template <int G, int Q> static __device__ void fix(uint32_t (&V)[NI][8]);",
@@ -530,8 +530,10 @@ def gen_pt(c: PsCodec):
     gf = c.gf
     for g, gitems in enumerate(R.groups):
         ws = [R.wfun[i] for i in gitems]
-        p0 = R.pieces[g][0] + R.pieces[g][1]            # wave (g, 0) = wave g
-        for pc in p0:
+        # every wave of group g runs its own pieces' networks (block index = absolute 8-position
+        # block), so no quarter needs a fix-up; fix<> stays for the shared-network variant
+        pall = sorted(set(p for w in range(W) if R.waves[w]["g"] == g for p in R.pieces[w][0] + R.pieces[w][1]))
+        for pc in pall:
             for B in (2 * pc, 2 * pc + 1):
                 emit_weight_block(out, f"template <> __device__ __forceinline__ void {st}::block<{g}, {B}>("
                                   "uint32_t (&V)[NI][8], const uint32_t (&X)[8])", ws, B)

@@ -950,14 +950,35 @@ __global__ void __launch_bounds__(64) k_bch_decode_wave(DevBch b, BchArgs a) {
     if (lane == 0) a.result[k] = res;
 }
 
+// The wavefront-per-codeword kernels take one workgroup per codeword: batches go in chunks of at
+// most kWaveChunk codewords, so the grid stays far below the 2^32-thread launch limit.
+constexpr size_t kWaveChunk = (size_t)1 << 24;
+
+BchArgs wave_chunk(const BchArgs &a, size_t k0) {
+    BchArgs c = a;
+    c.ncw = a.ncw - k0 < kWaveChunk ? a.ncw - k0 : kWaveChunk;
+    if (c.data) c.data += k0 * a.dstride;
+    if (c.wdata) c.wdata += k0 * a.dstride;
+    if (c.ecc) c.ecc += k0 * a.estride;
+    if (c.result) c.result += k0;
+    if (c.errloc) c.errloc += k0 * a.lstride;
+    if (c.syn) c.syn += k0 * a.sstride;
+    return c;
+}
+
 hipError_t launch_encode(const DevBch &b, BchArgs a, hipStream_t s) {
     if (b.nwl) {
-        const unsigned g = (unsigned)a.ncw;
-        if (b.nwl == 1) hipLaunchKernelGGL(k_bch_encode_wave<1>, dim3(g), dim3(64), 0, s, b, a);
-        else if (b.nwl == 2) hipLaunchKernelGGL(k_bch_encode_wave<2>, dim3(g), dim3(64), 0, s, b, a);
-        else if (b.nwl == 4) hipLaunchKernelGGL(k_bch_encode_wave<4>, dim3(g), dim3(64), 0, s, b, a);
-        else hipLaunchKernelGGL(k_bch_encode_wave<8>, dim3(g), dim3(64), 0, s, b, a);
-        return hipGetLastError();
+        for (size_t k0 = 0; k0 < a.ncw; k0 += kWaveChunk) {      // one workgroup per codeword
+            const BchArgs c = wave_chunk(a, k0);
+            const unsigned g = (unsigned)c.ncw;
+            if (b.nwl == 1) hipLaunchKernelGGL(k_bch_encode_wave<1>, dim3(g), dim3(64), 0, s, b, c);
+            else if (b.nwl == 2) hipLaunchKernelGGL(k_bch_encode_wave<2>, dim3(g), dim3(64), 0, s, b, c);
+            else if (b.nwl == 4) hipLaunchKernelGGL(k_bch_encode_wave<4>, dim3(g), dim3(64), 0, s, b, c);
+            else hipLaunchKernelGGL(k_bch_encode_wave<8>, dim3(g), dim3(64), 0, s, b, c);
+            const hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
     }
     const unsigned grid = (unsigned)((a.ncw + kThreads - 1) / kThreads);
     a.staged = want_staging(b, false, a);
@@ -972,13 +993,18 @@ hipError_t launch_encode(const DevBch &b, BchArgs a, hipStream_t s) {
 
 hipError_t launch_decode(const DevBch &b, BchArgs a, hipStream_t s) {
     if (b.nwl) {
-        const unsigned g = (unsigned)a.ncw;
         const size_t sh = wave_lds_bytes(b.t);
-        if (b.nwl == 1) hipLaunchKernelGGL(k_bch_decode_wave<1>, dim3(g), dim3(64), sh, s, b, a);
-        else if (b.nwl == 2) hipLaunchKernelGGL(k_bch_decode_wave<2>, dim3(g), dim3(64), sh, s, b, a);
-        else if (b.nwl == 4) hipLaunchKernelGGL(k_bch_decode_wave<4>, dim3(g), dim3(64), sh, s, b, a);
-        else hipLaunchKernelGGL(k_bch_decode_wave<8>, dim3(g), dim3(64), sh, s, b, a);
-        return hipGetLastError();
+        for (size_t k0 = 0; k0 < a.ncw; k0 += kWaveChunk) {      // one workgroup per codeword
+            const BchArgs c = wave_chunk(a, k0);
+            const unsigned g = (unsigned)c.ncw;
+            if (b.nwl == 1) hipLaunchKernelGGL(k_bch_decode_wave<1>, dim3(g), dim3(64), sh, s, b, c);
+            else if (b.nwl == 2) hipLaunchKernelGGL(k_bch_decode_wave<2>, dim3(g), dim3(64), sh, s, b, c);
+            else if (b.nwl == 4) hipLaunchKernelGGL(k_bch_decode_wave<4>, dim3(g), dim3(64), sh, s, b, c);
+            else hipLaunchKernelGGL(k_bch_decode_wave<8>, dim3(g), dim3(64), sh, s, b, c);
+            const hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
     }
     const unsigned grid = (unsigned)((a.ncw + kThreads - 1) / kThreads);
     a.staged = a.ecc_only ? 0 : want_staging(b, true, a);

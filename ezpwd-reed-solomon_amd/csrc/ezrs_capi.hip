@@ -220,6 +220,17 @@ int ezrs_destroy(ezrs_codec *c) {
     return 0;
 }
 
+int ezrs_set_semantics(ezrs_codec *c, int semantics) {
+    if (!c || (semantics != EZRS_SEM_EZPWD && semantics != EZRS_SEM_KARN)) return -EINVAL;
+    c->dev.karn = semantics == EZRS_SEM_KARN;
+    return 0;
+}
+
+int ezrs_get_semantics(const ezrs_codec *c) {
+    if (!c) return -EINVAL;
+    return c->dev.karn ? EZRS_SEM_KARN : EZRS_SEM_EZPWD;
+}
+
 int ezrs_kernel_path(const ezrs_codec *c) {
     if (!c) return -EINVAL;
     if (c->ps_id >= 0) return EZRS_PATH_PLANESLICE;
@@ -299,7 +310,9 @@ hipError_t dispatch_decode(const ezrs_codec *c, const DecodeArgs &a, uint8_t *sy
         return e;
     }
     if (a.sh.rows) return launch_decode_generic(c->dev, a, st);     // shard rows: per-codeword kernels
-    if (c->wide_id >= 0 && wide_can_decode(c->dev, a))
+    // the GF(2^16) error path keeps ezpwd's semantics only: Karn-mode codecs decode on the
+    // per-codeword kernels (same syndromes, Karn's frame and checks)
+    if (c->wide_id >= 0 && !c->dev.karn && wide_can_decode(c->dev, a))
         return launch_wide_decode(c->wide_id, c->dev, a, c->wide_blob.data(), c->d_wcols, syn_ws, st);
     if (c->bs_id >= 0 && contiguous) {
         // Bit-sliced syndromes for the whole batch; the reference algorithm only for the codewords
@@ -544,13 +557,15 @@ __global__ void __launch_bounds__(256) k_compact_rows(const int32_t *result, siz
     slot[threadIdx.x] = mine ? atomicAdd(ix, 1u) : 0xFFFFFFFFu;
     if (mine) ix[1 + slot[threadIdx.x]] = (uint32_t)k;
     __syncthreads();
-    // the block copies its flagged rows, 4 bytes per thread per step
-    for (int t = 0; t < 256; ++t) {
+    // the block copies its flagged rows, one row per wavefront at a time (4 rows in flight), a byte
+    // per lane per step (rows of any length and alignment; consecutive lanes, consecutive bytes)
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int t = wave; t < 256; t += 4) {
         const uint32_t sl = slot[t];
         if (sl == 0xFFFFFFFFu) continue;
         const char *src = rows + ((size_t)blockIdx.x * 256 + t) * row_bytes;
         char *dst = out + (size_t)sl * row_bytes;
-        for (size_t b = threadIdx.x; b < row_bytes; b += 256) dst[b] = src[b];
+        for (size_t b = lane; b < row_bytes; b += 64) dst[b] = src[b];
     }
 }
 

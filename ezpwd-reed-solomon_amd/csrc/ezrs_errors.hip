@@ -75,6 +75,10 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
                                                           uint8_t *corr_out, const uint8_t *syn_in,
                                                           unsigned syn_step) {
     const unsigned NR = c.nroots, LOAD = c.load, FCR = c.fcr, PRM = c.prim;
+    // Karn mode (c.karn): erasures and positions in the full 255 frame (decode_rs.h:114, 295) and
+    // none of ezpwd's extra failure checks
+    const bool karn = c.karn != 0;
+    const unsigned elim = karn ? 255u : len + NR;
     if (len == 0 || len > LOAD) return -1;                                    // 1375-1377
     if (no_eras > NR) return -1;                                              // 1380-1382
     // erasure positions (1383-1387): loaded four at a time where the row allows (all loads issued
@@ -95,7 +99,7 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
                         if (4u * c + q < no_eras) {
-                            bad |= x[q] >= len + NR;
+                            bad |= x[q] >= elim;
                             ep[(4 * c + q) * 64] = (uint8_t)x[q];
                         }
                     }
@@ -104,13 +108,14 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
         } else {
             for (unsigned i = 0; i < no_eras; ++i) {
                 const unsigned x = eras[i];
-                bad |= x >= len + NR;
+                bad |= x >= elim;
                 ep[i * 64] = (uint8_t)x;
             }
         }
         if (bad) return -1;
     }
     const unsigned pad = LOAD - len;
+    const unsigned epad = karn ? 0u : pad;    // frame offset of an erasure position
     auto S = [&](int k) -> uint16_t & { return W.srev[k * 64 + lane]; };
 
     // syndromes (polynomial form from the syndrome kernel; syndrome i at syn_in[i * syn_step]) ->
@@ -133,9 +138,9 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
 #pragma unroll
     for (int i = 0; i <= 32; ++i) lam[i] = i == 0;
     if (no_eras > 0) {
-        lam[1] = ga(L, (PRM * (c.nn - 1 - (W.root[lane] + pad))) % 255u);
+        lam[1] = ga(L, (PRM * (c.nn - 1 - (W.root[lane] + epad))) % 255u);
         for (unsigned e = 1; e < no_eras; ++e) {
-            const unsigned u = (PRM * (c.nn - 1 - (W.root[e * 64 + lane] + pad))) % 255u;
+            const unsigned u = (PRM * (c.nn - 1 - (W.root[e * 64 + lane] + epad))) % 255u;
             // lam[j] ^= lam[j-1] * alpha^u for j = e+1 .. 1 (lam[j-1] == 0 for j - 1 > e)
 #pragma unroll
             for (int j0 = 32; j0 >= 0; j0 -= 4) {
@@ -238,7 +243,7 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
             if (done) break;
         }
     }
-    if ((int)deg != count || deg == 0) count = -1;                           // 1577-1595
+    if ((int)deg != count || (deg == 0 && !karn)) count = -1;                // 1577-1595 (Karn: 0)
 
     if (count > 0) {
         // Omega = S * lambda mod x^(deg lambda), index form (1596-1604)
@@ -279,12 +284,18 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
                     }
                 }
             }
-            if (den == 0) { count = -1; break; }
+            // Karn applies den == 0 (log A0 = NN: the correction is num1 * num2) and skips a root
+            // in the pad (decode_rs.h:277-289); ezpwd fails both (1625-1648)
+            if (den == 0 && !karn) { count = -1; break; }
             if (num1 != 0) {
                 const unsigned loc = (rj * c.iprim + 254u) % 255u;
-                if (loc < pad) { count = -1; break; }
+                if (loc < pad) {
+                    if (karn) continue;
+                    count = -1;
+                    break;
+                }
                 const unsigned n2 = (unsigned)(((int)rj * ((int)FCR - 1)) % 255 + 255) % 255u;
-                const unsigned cor = ga(L, (gi(L, num1) + n2 + 255u - gi(L, den)) % 255u);
+                const unsigned cor = ga(L, (gi(L, num1) + n2 + (den ? 255u - gi(L, den) : 0u)) % 255u);
                 if (!c.dual) {
                     S(nrec++) = (uint16_t)(loc << 8 | cor);
                     if (corr_out) corr_out[j] = (uint8_t)cor;
@@ -329,7 +340,7 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
     }
     if (pos_out && count > 0)
         for (int i = 0; i < count; ++i)
-            pos_out[i] = (W.root[i * 64 + lane] * c.iprim + 254u) % 255u - pad;
+            pos_out[i] = (W.root[i * 64 + lane] * c.iprim + 254u) % 255u - (karn ? 0u : pad);
     return count;
 }
 

@@ -181,14 +181,18 @@ __device__ int decode_one(const DevCodec &c, const uint16_t *__restrict__ A,
                           const SY *syn_in = nullptr, W *lds = nullptr) {
     const unsigned NR = c.nroots, NN = c.nn, A0 = c.nn, mm = c.mm, LOAD = c.load;
     const unsigned FCR = c.fcr, PRM = c.prim;
+    // Karn mode (c.karn): erasures and positions in the full NN frame (decode_rs.h:114, 295), the
+    // datum is the symbol (no masked-path rules), and none of ezpwd's extra failure checks
+    const bool karn = c.karn != 0, masked = c.masked && !karn;
     if (len == 0 || len > LOAD) return -1;                                    // 1375-1377
     if (no_eras > NR) return -1;                                              // 1380-1382
     for (unsigned i = 0; i < no_eras; ++i)
-        if (eras[i] >= len + NR) return -1;                                   // 1383-1387
-    if (c.masked)
+        if (eras[i] >= (karn ? NN : len + NR)) return -1;                     // 1383-1387
+    if (masked)
         for (unsigned i = 0; i < NR; ++i)
             if (static_cast<unsigned>(parity[i]) & ~NN) return -1;            // 1215-1218
     const unsigned pad = LOAD - len;
+    const unsigned epad = karn ? 0u : pad;    // frame offset of an erasure position
 
     constexpr int kS = WS ? WS : 1;
     constexpr int kW = MAXR + 1;       // elements per working array
@@ -243,9 +247,9 @@ __device__ int decode_one(const DevCodec &c, const uint16_t *__restrict__ A,
     for (unsigned i = 0; i <= NR; ++i) lambda[(i) * kS] = 0;                        // 1436-1450
     lambda[(0) * kS] = 1;
     if (no_eras > 0) {
-        lambda[(1) * kS] = A[modnn(PRM * (NN - 1 - (eras[0] + pad)), NN, mm)];
+        lambda[(1) * kS] = A[modnn(PRM * (NN - 1 - (eras[0] + epad)), NN, mm)];
         for (unsigned i = 1; i < no_eras; ++i) {
-            const unsigned u = modnn(PRM * (NN - 1 - (eras[i] + pad)), NN, mm);
+            const unsigned u = modnn(PRM * (NN - 1 - (eras[i] + epad)), NN, mm);
             for (unsigned j = i + 1; j > 0; --j) {
                 const unsigned tmp = I[lambda[(j - 1) * kS]];
                 if (tmp != A0) lambda[(j) * kS] ^= A[modnn(u + tmp, NN, mm)];
@@ -331,7 +335,8 @@ __device__ int decode_one(const DevCodec &c, const uint16_t *__restrict__ A,
             if (++count == (int)deg_lambda) break;
         }
     }
-    if ((int)deg_lambda != count || deg_lambda == 0) { count = -1; goto finish; }   // 1577-1595
+    if ((int)deg_lambda != count || (deg_lambda == 0 && !karn)) { count = -1; goto finish; }   // 1577-1595
+    if (count == 0) goto finish;              // Karn: deg lambda = 0 decodes to 0 (decode_rs.h:232-240)
 
     nroot = (unsigned)count;
     if constexpr (MAXR > 32)
@@ -354,9 +359,15 @@ __device__ int decode_one(const DevCodec &c, const uint16_t *__restrict__ A,
         const unsigned top = deg_lambda < NR - 1 ? deg_lambda : NR - 1;
         for (int i = (int)(top & ~1u); i >= 0; i -= 2)
             if (lambda[(i + 1) * kS] != A0) den ^= A[modnn(lambda[(i + 1) * kS] + (unsigned)i * rj, NN, mm)];
-        if (den == 0) { count = -1; goto finish; }
+        // Karn applies den == 0 (its log is A0 = NN: the correction is num1 * num2) and skips a
+        // root in the pad (decode_rs.h:277-289); ezpwd fails both (1625-1648)
+        if (den == 0 && !karn) { count = -1; goto finish; }
         if (num1 != 0) {
-            if (locof(j) < pad) { count = -1; goto finish; }
+            if (locof(j) < pad) {
+                if (karn) continue;
+                count = -1;
+                goto finish;
+            }
             const unsigned cor = A[modnn(I[num1] + I[num2] + NN - I[den], NN, mm)];
             unsigned cv = cor;
             unsigned at, delta = cor;
@@ -385,7 +396,7 @@ __device__ int decode_one(const DevCodec &c, const uint16_t *__restrict__ A,
     }
 
 finish:
-    if (!c.masked || count > 0)   // roots are distinct, so the fixes commute
+    if (!masked || count > 0)     // roots are distinct, so the fixes commute
         for (unsigned j = 0; j < nroot; ++j) {
             if (!has_wrote(j)) continue;
             const unsigned l = locof(j);
@@ -396,7 +407,7 @@ finish:
         for (unsigned j = 0; j < nroot; ++j)
             if (has_wrote(j)) corr_out[j] = static_cast<T>(corrv[(j) * kS]);
     if (pos_out && count > 0)
-        for (int i = 0; i < count; ++i) pos_out[i] = locof(i) - pad;
+        for (int i = 0; i < count; ++i) pos_out[i] = locof(i) - (karn ? 0u : pad);
     return count;
 }
 

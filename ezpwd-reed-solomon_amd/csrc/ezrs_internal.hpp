@@ -28,6 +28,9 @@ struct DevCodec {
     int dual;
     int masked;                   // symbol narrower than its datum (rs_base:1194)
     int ncu;                      // compute units of the device (persistent grids)
+    int karn;                     // decode with Phil Karn's libfec semantics (ezrs_set_semantics):
+                                  // erasures and positions in the full NN frame, none of ezpwd's
+                                  // extra failure checks (fec-3.0.1/decode_rs.h:71-298)
     const uint16_t *alpha_to;     // device, nn+1
     const uint16_t *index_of;     // device, nn+1
     const uint16_t *genpoly;      // device, nroots+1 (index form)

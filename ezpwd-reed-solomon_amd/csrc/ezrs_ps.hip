@@ -36,6 +36,8 @@
 //     next chunk's workspace loads in flight during the map): 0.149 vs 0.144 ms.
 //
 #include "ezrs_internal.hpp"
+
+#include <atomic>
 #include "gen/ezrs_ps_tables.inc"
 
 namespace ezrs {
@@ -328,9 +330,17 @@ __device__ __forceinline__ void read_rows_shard(u32x4 (&R)[4], uint32_t lbuf, in
     }
 }
 
-template <class C, int G, int HI, bool SH>
-__device__ __forceinline__ void lin_pass(uint32_t (&V)[C::NI][8], uint32_t lbuf, uint32_t stride, int q, int lo,
+// Quarter Q's pieces.  Default: each piece runs its own networks (block index = its absolute
+// 8-position block).  EZRS_PT_SHARED_NETS (variant builds): quarter 0's networks on every quarter,
+// then fix<G, Q> multiplies the partials by alpha^(-16 Q e) (smaller code, more VALU).
+template <class C, int G, int Q, int HI, bool SH>
+__device__ __forceinline__ void lin_pass(uint32_t (&V)[C::NI][8], uint32_t lbuf, uint32_t stride, int lo,
                                          const uint32_t (&ph)[4], int tail_lo) {
+#ifdef EZRS_PT_SHARED_NETS
+    constexpr int BQ = 0;
+#else
+    constexpr int BQ = Q;
+#endif
     constexpr int NP = C::NP0[G] + C::NP1[G];
     u32x4 e = {0, 0, 0, 0};
     if constexpr (SH)
@@ -339,8 +349,8 @@ __device__ __forceinline__ void lin_pass(uint32_t (&V)[C::NI][8], uint32_t lbuf,
         constexpr int I = decltype(Ic)::value;
         constexpr int p0 = C::PIECE[G][I];
         if constexpr (16 * p0 < HI) {
-            const int pa = 16 * (p0 + q);
-            if (pa < HI) {                                   // wave-uniform
+            constexpr int pa = 16 * (p0 + Q);
+            if constexpr (pa < HI) {
                 u32x4 R[4];
                 if constexpr (SH) read_rows_shard(R, lbuf, pa, tail_lo, e);
                 else read_rows_lin(R, lbuf, stride, pa, lo, ph);
@@ -351,14 +361,14 @@ __device__ __forceinline__ void lin_pass(uint32_t (&V)[C::NI][8], uint32_t lbuf,
                     transpose4x4(c0, X);
                     transpose4x4(c1, X + 4);
                 }
-                block8_rt<C, G, HI, 2 * p0>(V, X, pa, lo);
+                block8_rt<C, G, HI, 2 * (p0 + BQ)>(V, X, pa, lo);
                 {
                     const uint32_t c2[4] = {R[0].z, R[1].z, R[2].z, R[3].z};
                     const uint32_t c3[4] = {R[0].w, R[1].w, R[2].w, R[3].w};
                     transpose4x4(c2, X);
                     transpose4x4(c3, X + 4);
                 }
-                block8_rt<C, G, HI, 2 * p0 + 1>(V, X, pa + 8, lo);
+                block8_rt<C, G, HI, 2 * (p0 + BQ) + 1>(V, X, pa + 8, lo);
             }
         }
     });
@@ -373,7 +383,9 @@ __device__ __forceinline__ void wave_tail_lin(uint32_t (&V)[C::NI][8], const PsA
     (void)pt_it; (void)pt_w;
     constexpr int G = W % C::GN, Q = W / C::GN;
     if (!(a.ablate & 2)) {
+#ifdef EZRS_PT_SHARED_NETS
         if constexpr (Q > 0) C::template fix<G, Q>(V);      // quarter 0's weights -> this quarter's
+#endif
         exchange<C, W, 0>(V, lbuf + 16u * fresh());         // slot (W XCAP + j) at 2 KiB each
     }
     PT_STAMP(4);
@@ -457,8 +469,10 @@ __device__ __forceinline__ void wave_tail_lin(uint32_t (&V)[C::NI][8], const PsA
     PT_STAMP(6);
 }
 
-template <class C, bool ENC, int G, bool SH>
-__device__ __forceinline__ void pt_run_lin(const PsArgs &a, uint8_t *lds, int w) {
+template <class C, bool ENC, int W, bool SH>
+__device__ __forceinline__ void pt_run_lin(const PsArgs &a, uint8_t *lds) {
+    constexpr int G = W % C::GN, Q = W / C::GN;
+    const int w = W;
     constexpr int HI = ENC ? kN - (int)C::NR : kN;
     const pw_rsrc_t rsrc = pw_rsrc(a.base, a.span);
     const uint32_t lbuf = __builtin_amdgcn_readfirstlane(lds_addr(lds));
@@ -485,8 +499,8 @@ __device__ __forceinline__ void pt_run_lin(const PsArgs &a, uint8_t *lds, int w)
     (void)pt_it; (void)pt_w;
     for (; tile < a.ntiles; tile += gridDim.x, ++pt_it) {
         // run-time values re-read each tile: nothing derived from them is hoisted out of the loop
-        int q = w / C::GN, lo = a.lo;
-        asm volatile("" : "+s"(q), "+s"(lo));
+        int lo = a.lo;
+        asm volatile("" : "+s"(lo));
         uint32_t ph[4];                                      // byte phase of row k's start
 #pragma unroll
         for (int k = 0; k < 4; ++k) ph[k] = (lbuf + kGuard + k * a.stride - (uint32_t)lo) & 3u;
@@ -538,23 +552,14 @@ __device__ __forceinline__ void pt_run_lin(const PsArgs &a, uint8_t *lds, int w)
             const uint32_t t0 = tile * kTile, kt = (t0 / a.srows) * a.srows + a.srows - 1;
             if (kt < t0 + kTile && kt < a.ncw) tlo = a.stail_lo;
         }
-        if (!(a.ablate & 1)) lin_pass<C, G, HI, SH>(V, lbuf, a.stride, q, lo, ph, tlo);
+        if (!(a.ablate & 1)) lin_pass<C, G, Q, HI, SH>(V, lbuf, a.stride, lo, ph, tlo);
 #if EZRS_PT_PRIO
         asm volatile("s_setprio 0");
 #endif
         PT_STAMP(2);
         barrier();                                           // the image is consumed
         PT_STAMP(3);
-        switch (w / C::GN) {
-        case 0: wave_tail_lin<C, ENC, G>(V, a, lbuf, tile, noff, nbytes, rsrc, rout, rws, pt_it); break;
-        case 1: if constexpr (C::QN > 1) wave_tail_lin<C, ENC, G + C::GN>(V, a, lbuf, tile, noff, nbytes, rsrc, rout, rws, pt_it); break;
-        case 2: if constexpr (C::QN > 2) wave_tail_lin<C, ENC, G + 2 * C::GN>(V, a, lbuf, tile, noff, nbytes, rsrc, rout, rws, pt_it); break;
-        case 3: if constexpr (C::QN > 3) wave_tail_lin<C, ENC, G + 3 * C::GN>(V, a, lbuf, tile, noff, nbytes, rsrc, rout, rws, pt_it); break;
-        case 4: if constexpr (C::QN > 4) wave_tail_lin<C, ENC, G + 4 * C::GN>(V, a, lbuf, tile, noff, nbytes, rsrc, rout, rws, pt_it); break;
-        case 5: if constexpr (C::QN > 5) wave_tail_lin<C, ENC, G + 5 * C::GN>(V, a, lbuf, tile, noff, nbytes, rsrc, rout, rws, pt_it); break;
-        case 6: if constexpr (C::QN > 6) wave_tail_lin<C, ENC, G + 6 * C::GN>(V, a, lbuf, tile, noff, nbytes, rsrc, rout, rws, pt_it); break;
-        default: if constexpr (C::QN > 7) wave_tail_lin<C, ENC, G + 7 * C::GN>(V, a, lbuf, tile, noff, nbytes, rsrc, rout, rws, pt_it); break;
-        }
+        wave_tail_lin<C, ENC, W>(V, a, lbuf, tile, noff, nbytes, rsrc, rout, rws, pt_it);
         toff = noff;
         tbytes = nbytes;
     }
@@ -569,8 +574,16 @@ k_pt_lin(PsArgs a) {
     static_assert(8 * C::XCAP * 2048 <= kLds, "exchange area");
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLds];
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (C::GN == 1 || w % C::GN == 0) pt_run_lin<C, ENC, 0, SH>(a, lds, w);
-    else pt_run_lin<C, ENC, C::GN - 1, SH>(a, lds, w);
+    switch (w) {                                             // each wave's pieces and tail, compiled
+    case 0: pt_run_lin<C, ENC, 0, SH>(a, lds); break;
+    case 1: pt_run_lin<C, ENC, 1, SH>(a, lds); break;
+    case 2: pt_run_lin<C, ENC, 2, SH>(a, lds); break;
+    case 3: pt_run_lin<C, ENC, 3, SH>(a, lds); break;
+    case 4: pt_run_lin<C, ENC, 4, SH>(a, lds); break;
+    case 5: pt_run_lin<C, ENC, 5, SH>(a, lds); break;
+    case 6: pt_run_lin<C, ENC, 6, SH>(a, lds); break;
+    default: pt_run_lin<C, ENC, 7, SH>(a, lds); break;
+    }
 }
 
 } // namespace pt
@@ -698,10 +711,16 @@ int planeslice_codec_id(const DevCodec &d) {
     return found;
 }
 
-// Timing experiments only: EZRS_PT_ABLATE disables phases of the tile kernel (PsArgs::ablate).
+// Timing experiments only: EZRS_PT_ABLATE disables phases of the tile kernel (PsArgs::ablate).  Read
+// only by variant builds compiled with -DEZRS_PT_ABLATE_ENV (tools/build_variant.sh); the release
+// library never looks at the environment here, so a stray variable cannot switch correction off.
 static int pt_ablate() {
+#ifdef EZRS_PT_ABLATE_ENV
     const char *e = getenv("EZRS_PT_ABLATE");
     return e ? atoi(e) : 0;
+#else
+    return 0;
+#endif
 }
 
 // Workspace: decode tiled syndromes (kSynTile); encode [NR][ws_pitch] syndromes, ws_pitch = ncw
@@ -711,11 +730,28 @@ size_t ps_ws_bytes(size_t ncw) { return ps_pitch(ncw) * 32; }
 
 // Largest batch one launch takes: every buffer offset stays below 0xF0000000 (32-bit offsets;
 // the tile kernel's out-of-range marker kOob is above them).
-static size_t ps_max_rows(size_t stride) { return ((size_t)0xE0000000u / stride) / 2048 * 2048; }
+// That covers the rows' span AND the per-codeword buffers: the result array (4 B per codeword) and
+// the syndrome workspace (32 B per codeword in either layout), so a short row pitch cannot wrap the
+// workspace offsets.  ezrs_set_launch_rows() lowers the cap (tests: launches split mid-batch and,
+// for shard batches, mid-tile; the results are the same by construction).
+static std::atomic<size_t> g_launch_rows{0};
+static size_t ps_row_cap() {
+    const size_t hard = (size_t)0xE0000000u / 32;
+    const size_t t = g_launch_rows.load(std::memory_order_relaxed);
+    return t && t < hard ? t : hard;
+}
+static size_t ps_max_rows(size_t stride) {
+    const size_t cap = ps_row_cap();
+    size_t m = (size_t)0xE0000000u / stride;
+    if (m > cap) m = cap;
+    return m >= 2048 && cap == (size_t)0xE0000000u / 32 ? m / 2048 * 2048 : m;   // a test cap: as set
+}
 
 // Shard batches: rows per launch, whole shards (byte offsets stay below 0xE0000000 as above).
 static size_t ps_max_rows_shards(const Shards &g) {
-    const size_t n = (size_t)0xE0000000u / g.pitch;
+    size_t n = (size_t)0xE0000000u / g.pitch;
+    const size_t byrows = ps_row_cap() / g.rows;
+    if (byrows < n) n = byrows;
     return (n ? n : 1) * g.rows;
 }
 
@@ -828,3 +864,8 @@ hipError_t launch_ps_syndromes(int id, const DevCodec &d, const DecodeArgs &a, u
 }
 
 } // namespace ezrs
+
+extern "C" int ezrs_set_launch_rows(size_t rows) {
+    ezrs::g_launch_rows.store(rows, std::memory_order_relaxed);
+    return 0;
+}

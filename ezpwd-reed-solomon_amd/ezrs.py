@@ -93,6 +93,9 @@ def lib():
         L.ezrs_decode_shards.argtypes = [_vp, _vp, _sz, _sz, _u, _sz, _vp, _sz, _vp, _vp, _vp, _sz,
                                          _vp, _sz, _vp]
         L.ezrs_kernel_path.argtypes = [_vp]
+        L.ezrs_set_launch_rows.argtypes = [_sz]
+        L.ezrs_set_semantics.argtypes = [_vp, _i]
+        L.ezrs_get_semantics.argtypes = [_vp]
         L.ezrs_host_alloc.argtypes = [C.POINTER(_vp), _sz]
         L.ezrs_host_free.argtypes = [_vp]
         L.ezbch_last_error.restype = C.c_char_p
@@ -110,6 +113,12 @@ def lib():
         L.ezbch_decode_host.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _vp, _vp, _sz, _sz, _sz]
         _lib = L
     return _lib
+
+
+def set_launch_rows(rows):
+    """Test hook (ezrs_set_launch_rows): cap the codewords one plane-sliced launch takes; 0 = the
+    default.  Results never depend on it."""
+    lib().ezrs_set_launch_rows(int(rows))
 
 
 def _check(rc, what, bch=False):
@@ -227,6 +236,16 @@ class Codec:
         """'generic' | 'bitslice' | 'planeslice' | 'wide' (ezrs_kernel_path)."""
         return ("generic", "bitslice", "planeslice", "wide")[_check(lib().ezrs_kernel_path(self._h),
                                                                       "ezrs_kernel_path")]
+
+    @property
+    def semantics(self):
+        """'ezpwd' (decode_symbols, the default) or 'karn' (libfec decode_rs_*: full-NN-frame
+        erasures and positions, none of ezpwd's extra failure checks) -- ezrs_set_semantics."""
+        return ("ezpwd", "karn")[_check(lib().ezrs_get_semantics(self._h), "ezrs_get_semantics")]
+
+    @semantics.setter
+    def semantics(self, mode):
+        _check(lib().ezrs_set_semantics(self._h, {"ezpwd": 0, "karn": 1}[mode]), "ezrs_set_semantics")
 
     def reserve(self, ncw, stream=None):
         """Pre-size the workspace of `stream` (default: the current torch stream)."""

@@ -88,6 +88,24 @@ int ezrs_destroy(ezrs_codec *codec);
 #define EZRS_PATH_PLANESLICE 2  /* plane-sliced GF(2^8) tile kernels (RS(255,K), NROOTS <= 32)       */
 #define EZRS_PATH_WIDE 3        /* GF(2^16) remainder-network kernels (RS(65535,65503/65519))        */
 int ezrs_kernel_path(const ezrs_codec *codec);
+/* Decode semantics of a codec (encode is the same under both):
+ *   EZRS_SEM_EZPWD (default) -- decode_symbols of c++/ezpwd/rs_base:1335-1718: erasures and
+ *     positions relative to the first supplied symbol; -1 for deg lambda = 0, a zero Forney
+ *     denominator or a root in the pad (rs_base:1589-1648).
+ *   EZRS_SEM_KARN -- decode_rs_char / decode_rs_int of Phil Karn's libfec
+ *     (fec-3.0.1/decode_rs.h:71-298): erasures and positions in the full NN frame (a position
+ *     p >= pad is row symbol p - pad), none of those three checks (a zero denominator applies
+ *     num1 * num2, a root in the pad is counted and reported but not corrected), the datum is the
+ *     symbol.  The Karn ABI (include/ezrs_fec.h) creates its codecs in this mode. */
+#define EZRS_SEM_EZPWD 0
+#define EZRS_SEM_KARN 1
+int ezrs_set_semantics(ezrs_codec *codec, int semantics);
+int ezrs_get_semantics(const ezrs_codec *codec);
+/* Test hook: cap the codewords one plane-sliced kernel launch takes (0 restores the default, the
+ * largest batch whose 32-bit buffer offsets fit).  Results never depend on it: lowering it only
+ * splits a batch over more launches (mid-tile for shard batches), which the tests use to exercise
+ * those splits at small sizes.  Process-wide; not for use while other threads launch. */
+int ezrs_set_launch_rows(size_t rows);
 int ezrs_get_info(const ezrs_codec *codec, ezrs_info *info);
 
 /* Pre-size the workspace of `stream` (NULL: the null stream) for batches of up to `ncw` codewords,

@@ -28,6 +28,7 @@ struct ezo_codec {
     uint16_t *alpha_to; /* nn+1 entries; alpha_to[nn] = 0           (rs_base:613-621) */
     uint16_t *index_of; /* nn+1 entries; index_of[0] = nn (A0)      (rs_base:613-621) */
     uint16_t *genpoly;  /* nroots+1 entries, index form             (rs_base:1263-1285) */
+    int karn;           /* decode with libfec's semantics (ezo_set_karn)               */
 };
 
 /* ------------------------------------------------------------------------------------------ */
@@ -151,12 +152,16 @@ static int decode_symbols(const ezo_codec *c, uint16_t *data, unsigned len, uint
     const unsigned FCR = c->fcr, PRM = c->prim;
     const uint16_t *alpha_to = c->alpha_to, *index_of = c->index_of;
     const int DUAL = c->dual;
+    /* Karn mode (fec-3.0.1/decode_rs.h:71-298): erasures and positions in the full NN frame
+     * (decode_rs.h:114, 295); none of ezpwd's checks of deg lambda = 0, den = 0 and roots in the
+     * pad (decode_rs.h:232-289) */
+    const int KARN = c->karn;
     if (len == 0 || len > LOAD) return -1;                               /* 1375-1377 */
-    unsigned pad = LOAD - len;
+    unsigned pad = LOAD - len, epad = KARN ? 0 : pad;
     if (no_eras) {                                                       /* 1379-1388 */
         if (no_eras > NR) return -1;
         for (unsigned i = 0; i < no_eras; ++i)
-            if (eras_pos[i] >= len + NR) return -1;
+            if (eras_pos[i] >= (KARN ? NN : len + NR)) return -1;
     }
 
     /* scratch: lambda, b, t, omega, reg (NR+1 each), syn (NR), root, loc (NR unsigned) */
@@ -192,9 +197,9 @@ static int decode_symbols(const ezo_codec *c, uint16_t *data, unsigned len, uint
 
     lambda[0] = 1;                                                       /* 1436-1450 */
     if (no_eras > 0) {
-        lambda[1] = alpha_to[modnn(c, PRM * (NN - 1 - (eras_pos[0] + pad)))];
+        lambda[1] = alpha_to[modnn(c, PRM * (NN - 1 - (eras_pos[0] + epad)))];
         for (unsigned i = 1; i < no_eras; i++) {
-            uint16_t u = (uint16_t)modnn(c, PRM * (NN - 1 - (eras_pos[i] + pad)));
+            uint16_t u = (uint16_t)modnn(c, PRM * (NN - 1 - (eras_pos[i] + epad)));
             for (unsigned j = i + 1; j > 0; j--) {
                 uint16_t tmp = index_of[lambda[j - 1]];
                 if (tmp != A0) lambda[j] ^= alpha_to[modnn(c, u + tmp)];
@@ -249,7 +254,7 @@ static int decode_symbols(const ezo_codec *c, uint16_t *data, unsigned len, uint
         if (++count == (int)deg_lambda) break;
     }
     if ((int)deg_lambda != count) { count = -1; goto finish; }
-    if (deg_lambda == 0) { count = -1; goto finish; }                    /* 1589-1595 */
+    if (deg_lambda == 0) { count = KARN ? 0 : -1; goto finish; }         /* 1589-1595 */
 
     deg_omega = deg_lambda - 1;                                          /* 1596-1604 */
     for (unsigned i = 0; i <= deg_omega; i++) {
@@ -269,9 +274,13 @@ static int decode_symbols(const ezo_codec *c, uint16_t *data, unsigned len, uint
         unsigned top = deg_lambda < NR - 1 ? deg_lambda : NR - 1;
         for (int i = (int)(top & ~1u); i >= 0; i -= 2)
             if (lambda[i + 1] != A0) den ^= alpha_to[modnn(c, lambda[i + 1] + (unsigned)i * root[j])];
-        if (den == 0) { count = -1; goto finish; }
+        if (den == 0 && !KARN) { count = -1; goto finish; }   /* Karn: index_of[0] = A0 = NN */
         if (num1 != 0) {
-            if (loc[j] < pad) { count = -1; goto finish; }
+            if (loc[j] < pad) {
+                if (KARN) continue;                                      /* not corrected */
+                count = -1;
+                goto finish;
+            }
             uint16_t cor = alpha_to[modnn(c, index_of[num1] + index_of[num2] + NN - index_of[den])];
             if (corr) corr[j] = cor;
             if (loc[j] < NN - NR) {
@@ -301,7 +310,7 @@ static int decode_symbols(const ezo_codec *c, uint16_t *data, unsigned len, uint
 
 finish:                                                                  /* 1713-1717 */
     if (eras_pos != NULL)
-        for (int i = 0; i < count; i++) eras_pos[i] = loc[i] - pad;
+        for (int i = 0; i < count; i++) eras_pos[i] = loc[i] - (KARN ? 0 : pad);
     if (s16 != sbuf) free(s16);
     if (u32 != ubuf) free(u32);
     return count;
@@ -335,7 +344,7 @@ int ezo_decode(const ezo_codec *c, void *data, unsigned len, void *parity, unsig
                unsigned no_eras, void *corr) {
     const unsigned NR = c->nroots, LOAD = c->nn - c->nroots, w = c->datum;
     if (len < 1 || parity == NULL) return -1;                            /* 1180-1182 */
-    const int masked = c->mm != 8 * w;                                   /* 1194 */
+    const int masked = c->mm != 8 * w && !c->karn;                       /* 1194 */
     uint16_t tmp[65536], ctmp[65536];
     if (len > LOAD) return -1;  /* decode_symbols rejects it; never index tmp past LOAD */
     uint16_t *dp = tmp, *pp = tmp + len;
@@ -403,3 +412,6 @@ int ezo_decode_batch(const ezo_codec *c, void *data, size_t data_stride, unsigne
     }
     return 0;
 }
+
+/* Karn mode on (1) / off (0): decode with fec-3.0.1's semantics (see decode_symbols). */
+void ezo_set_karn(ezo_codec *c, int karn) { c->karn = karn ? 1 : 0; }

@@ -57,6 +57,9 @@ int ezo_decode(const ezo_codec *c, void *data, unsigned len, void *parity, unsig
  * pos_stride >= NROOTS entries, corr (nullable) rows of corr_stride >= NROOTS datums. */
 int ezo_encode_batch(const ezo_codec *c, const void *data, size_t data_stride, unsigned len,
                      void *parity, size_t parity_stride, size_t ncw, int nthreads);
+/* Decode with Phil Karn's libfec semantics instead (fec-3.0.1/decode_rs.h:71-298): erasures and
+ * positions in the full NN frame, no failure for deg lambda = 0, den = 0 or a root in the pad. */
+void ezo_set_karn(ezo_codec *c, int karn);
 int ezo_decode_batch(const ezo_codec *c, void *data, size_t data_stride, unsigned len,
                      void *parity, size_t parity_stride, const uint32_t *eras, size_t eras_stride,
                      const uint32_t *neras, int32_t *result, uint32_t *positions,

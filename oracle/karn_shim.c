@@ -11,6 +11,34 @@
 #include <string.h>
 #include "fec.h"
 
+/* General-purpose int codec (fec.h as patched by phil-karn/fec-3.0.1-int.patch): unsigned int
+ * symbols, symsize up to 16.  Rows here are uint16 arrays (the engine's container for m > 8). */
+void *karn_init_int(int symsize, int gfpoly, int fcr, int prim, int nroots, int pad) {
+    return init_rs_int(symsize, gfpoly, fcr, prim, nroots, pad);
+}
+
+void karn_free_int(void *rs) { free_rs_int(rs); }
+
+void karn_encode_int_batch(void *rs, const uint16_t *data, long stride, uint16_t *parity, long pstride,
+                           long ncw, int len, int nroots) {
+    unsigned int buf[65536], par[65536];
+    for (long i = 0; i < ncw; ++i) {
+        for (int j = 0; j < len; ++j) buf[j] = data[i * stride + j];
+        encode_rs_int(rs, buf, par);
+        for (int j = 0; j < nroots; ++j) parity[i * pstride + j] = (uint16_t)par[j];
+    }
+}
+
+void karn_decode_int_batch(void *rs, uint16_t *rows, long stride, long ncw, int nroots, int rowlen, int *eras,
+                           const int *neras, int *result) {
+    static unsigned int buf[65536];
+    for (long i = 0; i < ncw; ++i) {
+        for (int j = 0; j < rowlen; ++j) buf[j] = rows[i * stride + j];
+        result[i] = decode_rs_int(rs, buf, eras + i * nroots, neras ? neras[i] : 0);
+        for (int j = 0; j < rowlen; ++j) rows[i * stride + j] = (uint16_t)buf[j];
+    }
+}
+
 /* General-purpose char codec (fec.h: init_rs_char / encode_rs_char / decode_rs_char). */
 void *karn_init_char(int symsize, int gfpoly, int fcr, int prim, int nroots, int pad) {
     return init_rs_char(symsize, gfpoly, fcr, prim, nroots, pad);

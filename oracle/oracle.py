@@ -56,6 +56,7 @@ def lib():
         L.ezo_encode_batch.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _sz, _i]
         L.ezo_decode_batch.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _vp, _sz, _vp, _vp, _vp,
                                        _sz, _vp, _sz, _sz, _i]
+        L.ezo_set_karn.argtypes = [_vp, _i]
         L.ezo_into_dual.restype = C.POINTER(C.c_uint8)
         L.ezo_from_dual.restype = C.POINTER(C.c_uint8)
         _lib = L
@@ -65,12 +66,14 @@ def lib():
 class Codec:
     """RS codec in the restatement: Codec(mm, poly, fcr, prim, nroots, dual)."""
 
-    def __init__(self, mm, poly, fcr, prim, nroots, dual=False):
+    def __init__(self, mm, poly, fcr, prim, nroots, dual=False, karn=False):
         self.mm, self.poly, self.fcr, self.prim, self.nroots, self.dual = (
             mm, poly, fcr, prim, nroots, bool(dual))
         self._h = lib().ezo_create(mm, poly, fcr, prim, nroots, int(bool(dual)))
         if not self._h:
             raise ValueError("invalid RS codec parameters")
+        if karn:      # decode with libfec's semantics (ezrs_oracle.c decode_symbols)
+            lib().ezo_set_karn(self._h, 1)
         self.nn = (1 << mm) - 1
         self.load = self.nn - nroots
         self.dtype = np.uint8 if mm <= 8 else np.uint16
@@ -259,6 +262,11 @@ class Karn:
             L.karn_free_char.argtypes = [_vp]
             L.karn_encode_char_batch.argtypes = [_vp, _vp, C.c_long, _vp, C.c_long, C.c_long, _i]
             L.karn_decode_char_batch.argtypes = [_vp, _vp, C.c_long, C.c_long, _i, _vp, _vp, _vp]
+            L.karn_init_int.restype = _vp
+            L.karn_init_int.argtypes = [_i, _i, _i, _i, _i, _i]
+            L.karn_free_int.argtypes = [_vp]
+            L.karn_encode_int_batch.argtypes = [_vp, _vp, C.c_long, _vp, C.c_long, C.c_long, _i, _i]
+            L.karn_decode_int_batch.argtypes = [_vp, _vp, C.c_long, C.c_long, _i, _i, _vp, _vp, _vp]
             for f in ("karn_encode_8_batch", "karn_encode_ccsds_batch"):
                 getattr(L, f).argtypes = [_vp, C.c_long, _vp, C.c_long, C.c_long, _i]
             for f in ("karn_decode_8_batch", "karn_decode_ccsds_batch"):
@@ -288,6 +296,30 @@ class Karn:
         L.karn_decode_char_batch(rs, _ptr(rows), rows.shape[1], ncw, params[4], _ptr(eras), _ptr(neras),
                                  _ptr(result))
         L.karn_free_char(rs)
+        return result
+
+    @classmethod
+    def encode_int(cls, params, data, length):
+        """init_rs_int codec; data uint16 [ncw, >= length]; returns uint16 parity [ncw, nroots]."""
+        L = cls.lib()
+        rs = L.karn_init_int(*params)
+        assert rs, "init_rs_int rejected the parameters"
+        ncw = data.shape[0]
+        par = np.zeros((ncw, params[4]), np.uint16)
+        L.karn_encode_int_batch(rs, _ptr(data), data.shape[1], _ptr(par), par.shape[1], ncw, length, params[4])
+        L.karn_free_int(rs)
+        return par
+
+    @classmethod
+    def decode_int(cls, params, rows, eras, neras):
+        """rows uint16 [ncw, len + nroots] corrected in place; eras int32 [ncw, nroots] in/out."""
+        L = cls.lib()
+        rs = L.karn_init_int(*params)
+        ncw = rows.shape[0]
+        result = np.zeros(ncw, np.int32)
+        L.karn_decode_int_batch(rs, _ptr(rows), rows.shape[1], ncw, params[4], rows.shape[1], _ptr(eras),
+                                _ptr(neras), _ptr(result))
+        L.karn_free_int(rs)
         return result
 
     @classmethod

@@ -89,3 +89,28 @@ def test_bch_no_device_reports_enodev():
     assert L.ezbch_create(C.byref(h), 15, 200, 0, 0) == -errno.ENODEV
     with pytest.raises(ezrs.EzrsError):
         ezrs.BCH(8, 2)
+
+
+def test_fec_library_exports_every_declared_symbol():
+    """libezrs_fec.so (Phil Karn's libfec RS ABI over the engine) exports every function that
+    include/ezrs_fec.h declares (fec-3.0.1/fec.h:229-257, phil-karn/rs.h:22-23, batch forms)."""
+    import re
+    hdr = os.path.join(os.path.dirname(ezrs.HEADER), "ezrs_fec.h")
+    txt = open(hdr).read()
+    declared = set(re.findall(r"^\s*(?:int|void|void \*|ezrs_codec \*)\s*\*?\s*(\w+)\s*\(", txt, re.M))
+    assert {"init_rs_char", "decode_rs_int", "encode_rs_8", "decode_rs_ccsds", "pad_rs_char",
+            "decode_rs_char_batch", "ezrs_fec_codec"} <= declared
+    so = os.path.join(os.path.dirname(ezrs.LIB_PATH), "libezrs_fec.so")
+    out = subprocess.check_output(["nm", "-D", "--defined-only", so], text=True)
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    assert declared <= exported, declared - exported
+
+
+def test_fec_init_fails_without_device():
+    """No GPU: init_rs_char returns NULL (Karn's failure value); invalid parameters too."""
+    so = os.path.join(os.path.dirname(ezrs.LIB_PATH), "libezrs_fec.so")
+    L = C.CDLL(so)
+    L.init_rs_char.restype = C.c_void_p
+    assert not L.init_rs_char(8, 0x11d, 1, 1, 300, 0)        # nroots >= 2^symsize
+    assert not L.init_rs_char(8, 0x11d, 1, 1, 32, 223)       # pad leaves no data symbol
+    assert not L.init_rs_char(9, 0x211, 1, 1, 32, 0)         # char containers hold m <= 8

@@ -1,0 +1,168 @@
+"""Phil Karn's libfec RS ABI over the engine (include/ezrs_fec.h, libezrs_fec.so) against libfec's own
+outputs (tests/golden/karn_sem.npz, tests/golden/make_karn_sem_fixtures.py): every Tab row symbol
+size of phil-karn/rstest.c:26-50, shortened codewords, erasures in the pad and overwhelmed words
+(where Karn's decoder and ezpwd's differ).  Parity, results, corrected rows and positions -- in
+libfec's order, full NN frame -- are compared exactly, through the batch forms, the single-codeword
+calls and the device-batch API in Karn mode (ezrs_set_semantics)."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+import karn_sem_util as KS
+
+pytestmark = pytest.mark.gpu
+
+CASES = KS.cases()
+_vp, _sz, _i = C.c_void_p, C.c_size_t, C.c_int
+
+
+@pytest.fixture(scope="module")
+def fec():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import ezrs
+    L = C.CDLL(os.path.join(os.path.dirname(ezrs.LIB_PATH), "libezrs_fec.so"))
+    for f in ("init_rs_char", "init_rs_int"):
+        getattr(L, f).restype = _vp
+        getattr(L, f).argtypes = [_i] * 6
+    for f in ("free_rs_char", "free_rs_int"):
+        getattr(L, f).argtypes = [_vp]
+    for f in ("encode_rs_char_batch", "encode_rs_int_batch"):
+        getattr(L, f).argtypes = [_vp, _vp, _sz, _vp, _sz, _sz]
+    for f in ("decode_rs_char_batch", "decode_rs_int_batch"):
+        getattr(L, f).argtypes = [_vp, _vp, _sz, _vp, _sz, _vp, _vp, _sz]
+    L.encode_rs_char.argtypes = [_vp, _vp, _vp]
+    L.decode_rs_char.argtypes = [_vp, _vp, _vp, _i]
+    L.encode_rs_int.argtypes = [_vp, _vp, _vp]
+    L.decode_rs_int.argtypes = [_vp, _vp, _vp, _i]
+    for f in ("encode_rs_8", "encode_rs_ccsds"):
+        getattr(L, f).argtypes = [_vp, _vp, _i]
+    for f in ("decode_rs_8", "decode_rs_ccsds"):
+        getattr(L, f).argtypes = [_vp, _vp, _i, _i]
+    L.pad_rs_char.restype = _vp
+    L.pad_rs_char.argtypes = [_vp, _i]
+    L.ezrs_fec_codec.restype = _vp
+    L.ezrs_fec_codec.argtypes = [_vp]
+    return L
+
+
+def _p(a):
+    return a.ctypes.data_as(_vp)
+
+
+def _check_positions(res, pos, exp, nr):
+    for k in np.nonzero(res > 0)[0]:
+        np.testing.assert_array_equal(pos[k, :res[k]], exp[k, :res[k]], err_msg=f"positions cw {k}")
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c["kind"] in ("char", "int")], ids=lambda c: c["id"])
+def test_batch_forms_match_libfec(fec, case):
+    m, poly, fcr, prim, nr = case["params"]
+    pad, ints = case["pad"], case["kind"] == "int"
+    init = fec.init_rs_int if ints else fec.init_rs_char
+    rs = init(m, poly, fcr, prim, nr, pad)
+    assert rs, "init failed"
+    try:
+        dt = np.uint32 if ints else np.uint8
+        data = case["data"].astype(dt)
+        ncw, K = data.shape
+        par = np.zeros((ncw, nr), dt)
+        enc = fec.encode_rs_int_batch if ints else fec.encode_rs_char_batch
+        assert enc(rs, _p(data), K, _p(par), nr, ncw) == 0
+        np.testing.assert_array_equal(par, case["parity"].astype(dt))
+        rows = case["dec_in"].astype(dt)
+        eras = case["dec_eras"].astype(np.int32).copy()
+        neras = case["dec_neras"].astype(np.int32)
+        res = np.zeros(ncw, np.int32)
+        dec = fec.decode_rs_int_batch if ints else fec.decode_rs_char_batch
+        assert dec(rs, _p(rows), rows.shape[1], _p(eras), nr, _p(neras), _p(res), ncw) == 0
+        np.testing.assert_array_equal(res, case["dec_result"])
+        np.testing.assert_array_equal(rows, case["dec_out"].astype(dt))
+        _check_positions(res, eras, case["dec_positions"], nr)
+    finally:
+        (fec.free_rs_int if ints else fec.free_rs_char)(rs)
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: c["id"])
+def test_single_codeword_calls_match_libfec(fec, case):
+    """encode_rs_* / decode_rs_* one codeword at a time (48 per case, every Karn entry point)."""
+    m, poly, fcr, prim, nr = case["params"]
+    pad, kind = case["pad"], case["kind"]
+    ints = kind == "int"
+    dt = np.uint32 if ints else np.uint8
+    n = min(48, case["data"].shape[0])
+    rs = None
+    if kind in ("char", "int"):
+        rs = (fec.init_rs_int if ints else fec.init_rs_char)(m, poly, fcr, prim, nr, pad)
+        assert rs
+    try:
+        for k in range(n):
+            d = np.ascontiguousarray(case["data"][k].astype(dt))
+            p = np.zeros(nr, dt)
+            if kind == "char":
+                fec.encode_rs_char(rs, _p(d), _p(p))
+            elif kind == "int":
+                fec.encode_rs_int(rs, _p(d), _p(p))
+            else:
+                getattr(fec, f"encode_rs_{kind}")(_p(d), _p(p), pad)
+            np.testing.assert_array_equal(p, case["parity"][k].astype(dt), err_msg=f"parity cw {k}")
+            row = np.ascontiguousarray(case["dec_in"][k].astype(dt))
+            ne = int(case["dec_neras"][k])
+            ep = np.zeros(nr, np.int32)
+            ep[:ne] = case["dec_eras"][k, :ne]
+            if kind == "char":
+                r = fec.decode_rs_char(rs, _p(row), _p(ep), ne)
+            elif kind == "int":
+                r = fec.decode_rs_int(rs, _p(row), _p(ep), ne)
+            else:
+                r = getattr(fec, f"decode_rs_{kind}")(_p(row), _p(ep), ne, pad)
+            assert r == case["dec_result"][k], f"result cw {k}"
+            np.testing.assert_array_equal(row, case["dec_out"][k].astype(dt), err_msg=f"row cw {k}")
+            if r > 0:
+                np.testing.assert_array_equal(ep[:r], case["dec_positions"][k, :r], err_msg=f"positions cw {k}")
+    finally:
+        if rs:
+            (fec.free_rs_int if ints else fec.free_rs_char)(rs)
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c["params"][0] == 8], ids=lambda c: c["id"])
+def test_device_batches_in_karn_mode(fec, case):
+    """ezrs_decode on device tensors of a Karn-mode codec (ezrs.Codec.semantics = 'karn'): the
+    plane-sliced / bit-sliced syndrome kernels and the GF(2^8) error path under Karn's rules."""
+    import torch
+    import ezrs
+    m, poly, fcr, prim, nr = case["params"]
+    c = ezrs.Codec(m, poly, fcr, prim, nr, dual=case["kind"] == "ccsds")
+    c.semantics = "karn"
+    assert c.semantics == "karn"
+    K = case["data"].shape[1]
+    rows = torch.from_numpy(case["dec_in"].copy()).cuda()
+    eras = torch.from_numpy(case["dec_eras"].astype(np.int32)).cuda()
+    neras = torch.from_numpy(case["dec_neras"].astype(np.int32)).cuda()
+    pos = torch.zeros((rows.shape[0], nr), dtype=torch.int32, device="cuda")
+    res = c.decode(rows, K, None, eras=eras, neras=neras, positions=pos)
+    torch.cuda.synchronize()
+    res = res.cpu().numpy()
+    np.testing.assert_array_equal(res, case["dec_result"])
+    np.testing.assert_array_equal(rows.cpu().numpy(), case["dec_out"])
+    _check_positions(res, pos.cpu().numpy(), case["dec_positions"], nr)
+
+
+def test_pad_rs_changes_the_frame(fec):
+    """pad_rs_char (phil-karn/pad_rs.c): rejects a pad that leaves no data symbol, else re-pads."""
+    rs = fec.init_rs_char(8, 0x11d, 1, 1, 32, 0)
+    try:
+        assert not fec.pad_rs_char(rs, 223)
+        assert fec.pad_rs_char(rs, 100) == rs
+        case = next(c for c in CASES if c["kind"] == "char" and c["params"] == (8, 0x11d, 1, 1, 32) and c["pad"])
+        assert fec.pad_rs_char(rs, case["pad"]) == rs
+        d = np.ascontiguousarray(case["data"][0])
+        p = np.zeros(32, np.uint8)
+        fec.encode_rs_char(rs, _p(d), _p(p))
+        np.testing.assert_array_equal(p, case["parity"][0])
+        assert fec.ezrs_fec_codec(rs)
+    finally:
+        fec.free_rs_char(rs)

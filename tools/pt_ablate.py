@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Timing-only ablations of the tile kernel (EZRS_PT_ABLATE bits, see PsArgs::ablate): per variant,
 the device time of ezrs_encode and ezrs_decode on 1M RS(255,223) rows.  Results are garbage
-under ablation; nothing is checked.  Usage: python tools/pt_ablate.py [bits ...]"""
+under ablation; nothing is checked.  Needs a variant library built with the env hook:
+  tools/build_variant.sh ablate -DEZRS_PT_ABLATE_ENV, then EZRS_LIB_VARIANT=<path>.
+Usage: python tools/pt_ablate.py [bits ...]"""
 import os
 import sys
 
