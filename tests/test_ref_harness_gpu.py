@@ -58,11 +58,14 @@ def test_rstest_karn_abi():
     rc, out = _run("rstest", 600)
     assert rc == 0, out[-3000:]
     lines = out.splitlines()
-    assert "Testing fixed (255,223) RS codec...OK" in lines
-    assert "Testing CCSDS standard (255,223) RS codec...OK" in lines
+    # exercise.c's DEBUG=1 trial lines follow each "Testing ..." header; every codec then prints a
+    # line "OK" (rstest.c:77-79, 84-86, 111-113)
+    assert any(ln.startswith("Testing fixed (255,223) RS codec...") for ln in lines)
+    assert any(ln.startswith("Testing CCSDS standard (255,223) RS codec...") for ln in lines)
     tested = [ln for ln in lines if ln.startswith("Testing (")]
     assert len(tested) == 24, tested
+    assert sum(ln == "OK" for ln in lines) == 26, [ln for ln in lines if "OK" in ln][:30]
     bad = [ln for ln in lines if "decoder says" in ln or "without error" in ln or "uncorrected" in ln
            or "failed" in ln]
     assert not bad, "\n".join(bad[:20])
-    assert lines[-1] == "All codec tests passed!" or "All codec tests passed!" in lines
+    assert "All codec tests passed!" in lines
