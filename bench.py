@@ -41,6 +41,17 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def bench_device(local):
+    """This rank's GPU: LOCAL_RANK on a node with a GPU per rank; ranks beyond the visible GPUs wrap
+    around (a one-GPU box running --gpus 2 puts both ranks on cuda:0, which only the harness test
+    does).  The process group is gloo on CPU: the only cross-rank traffic is the barrier and the
+    scalar max/sum of the timing rule, so no RCCL communicator is ever needed."""
+    import torch
+    dev = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
+    return dev
+
+
 def host_cpu_info():
     """CPU model, logical CPUs (nproc), the CPUs this process may run on, the cgroup CPU quota
     and the physical core count of the host."""
@@ -241,9 +252,9 @@ def bench_rs_errors(args):
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    local = bench_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("gloo")
     c3 = args.workload == "c3"
     n, k = (255, 223) if c3 else (65535, 65503)
     ncw = args.ncw if (c3 or args.ncw != 1 << 20) else 65536     # C4: 64k codewords (configs[3])
@@ -301,7 +312,7 @@ def bench_rs_errors(args):
     torch.cuda.synchronize()
     enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
     dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
-    t = shard.max_over_ranks(enc_ms + dec_ms, device="cuda")
+    t = shard.max_over_ranks(enc_ms + dec_ms)
     row = n * w
     value = ncw * world * row / (t * 1e-3) / 1e9
     dom, ms, per = ("ezrs_encode", enc_ms, row) if enc_ms >= dec_ms else ("ezrs_decode", dec_ms, row + 4)
@@ -340,9 +351,9 @@ def bench_c5(args):
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    local = bench_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("gloo")
     c = ezrs.BCH.nkt(1023, 983, 4, device=local)
     ncw, L, row = args.ncw, 122, 127
     gen = torch.Generator(device="cuda").manual_seed(0x5EED0005 + rank)
@@ -389,7 +400,7 @@ def bench_c5(args):
     torch.cuda.synchronize()
     enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
     dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
-    t = shard.max_over_ranks(enc_ms + dec_ms, device="cuda")
+    t = shard.max_over_ranks(enc_ms + dec_ms)
     value = ncw * world * row / (t * 1e-3) / 1e9
     dom, ms, per = ("ezbch_encode", enc_ms, row) if enc_ms >= dec_ms else ("ezbch_decode", dec_ms, row + 4)
     achieved = ncw * per / (ms * 1e-3) / 1e9
@@ -470,6 +481,168 @@ def harness_check(args):
         dist.destroy_process_group()
 
 
+def shard_point(codec, S, steps, warmup, gen):
+    """One shard size of the sweep: ~256 MB of S-byte shards, encode_shards + decode_shards timed
+    with HIP events (one launch each), the rates and HBM fractions of both calls."""
+    import torch
+    shards = max(1, (256 << 20) // S)
+    R = codec.shard_codewords(S)
+    enc = codec.shard_encoded_len(S)
+    buf = torch.randint(0, 256, (shards, enc), generator=gen, device="cuda",
+                        dtype=torch.int32).to(torch.uint8)
+    codec.reserve(shards * R)
+    res = torch.empty(shards * R, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream()
+
+    def step(ev=None):
+        if ev:
+            ev[0].record(stream)
+        codec.encode_shards(buf, S, stream=stream)
+        if ev:
+            ev[1].record(stream)
+        codec.decode_shards(buf, S, result=res, stream=stream)
+        if ev:
+            ev[2].record(stream)
+    for _ in range(max(1, warmup)):
+        step()
+    torch.cuda.synchronize()
+    if int((res != 0).sum()):
+        raise SystemExit(f"shards S={S}: encoded shards did not decode clean")
+    steps = max(1, steps)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(evs[i])
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / steps
+    dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / steps
+    enc_alg = shards * enc                         # data read + parity written
+    dec_alg = enc_alg + 4 * shards * R             # all read + result written
+    return {"shard_bytes": S, "shards": shards, "codewords": shards * R,
+            "tail_len": S - (R - 1) * K, "gbs_shard_data": round(shards * S / dt / 1e9, 3),
+            "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4),
+            "frac_encode": round(enc_alg / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "frac_decode": round(dec_alg / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
+
+def timed_pair(enc_fn, dec_fn, steps, warmup, pre=None):
+    """Average HIP-event time (ms) of enc_fn and dec_fn on the current stream over `steps` steps;
+    pre() (outside the events) runs before each step."""
+    import torch
+    stream = torch.cuda.current_stream()
+    for _ in range(max(1, warmup)):
+        if pre:
+            pre()
+        enc_fn(stream)
+        dec_fn(stream)
+    torch.cuda.synchronize()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    for e in evs:
+        if pre:
+            pre()
+        e[0].record(stream)
+        enc_fn(stream)
+        e[1].record(stream)
+        dec_fn(stream)
+        e[2].record(stream)
+    torch.cuda.synchronize()
+    return (sum(e[0].elapsed_time(e[1]) for e in evs) / steps,
+            sum(e[1].elapsed_time(e[2]) for e in evs) / steps)
+
+
+def c2_extras(codec, args):
+    """The north_star / SURVEY 8(d) figures the driver's default run carries beside the headline
+    (all timed in the same process, HIP events): shard batches at S = 1 KiB and 1 MiB, C2 at 4M
+    codewords (1.07 GB, past the 256 MiB Infinity Cache), the C3 decode (8 errors + 4 erasures per
+    codeword), and the host-memory (PCIe-inclusive) rates, clean and with 1 % of the rows
+    corrupted.  None of these is `value`."""
+    import numpy as np
+    import torch
+    out = {}
+    gen = torch.Generator(device="cuda").manual_seed(0x5EED0007)
+    out["shards"] = {}
+    for S in (1 << 10, 1 << 20):
+        r = shard_point(codec, S, max(3, args.steps // 2), 1, gen)
+        out["shards"][f"{S // 1024}KiB"] = r
+        log(f"extras: shards S={S}: {r}")
+    torch.cuda.empty_cache()
+    # C2 at 4M codewords
+    n4 = 4 << 20
+    big = torch.randint(0, 256, (n4, N), generator=gen, device="cuda", dtype=torch.int32).to(torch.uint8)
+    codec.reserve(n4)
+    res4 = torch.empty(n4, dtype=torch.int32, device="cuda")
+    e_ms, d_ms = timed_pair(lambda st: codec.encode(big, K, stream=st),
+                            lambda st: codec.decode(big, K, result=res4, stream=st), 5, 1)
+    if int((res4 != 0).sum()):
+        raise SystemExit("C2 4M: encoded codewords did not decode clean")
+    out["c2_4m"] = {"codewords": n4, "encode_ms": round(e_ms, 4), "decode_ms": round(d_ms, 4),
+                    "value_gbs": round(n4 * N / ((e_ms + d_ms) * 1e-3) / 1e9, 3),
+                    "frac_encode": round(n4 * ENC_BYTES / (e_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                    "frac_decode": round(n4 * DEC_BYTES / (d_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    log(f"extras: c2_4m {out['c2_4m']}")
+    del big, res4
+    torch.cuda.empty_cache()
+    # C3: 1M codewords, 12 distinct corrupted symbols (positions b + j s mod 255, s coprime to 255),
+    # the last 4 passed as erasures; the corrupted master is copied in before each step (outside
+    # the events)
+    ncw = 1 << 20
+    clean = torch.randint(0, 256, (ncw, N), generator=gen, device="cuda", dtype=torch.int32).to(torch.uint8)
+    codec.encode(clean, K)
+    cop = torch.tensor([s_ for s_ in range(1, 255) if np.gcd(s_, 255) == 1], device="cuda")
+    b0 = torch.randint(0, 255, (ncw, 1), generator=gen, device="cuda")
+    st_ = cop[torch.randint(0, len(cop), (ncw, 1), generator=gen, device="cuda")]
+    locs = (b0 + torch.arange(12, device="cuda")[None, :] * st_) % 255
+    vals = torch.randint(1, 256, (ncw, 12), generator=gen, device="cuda", dtype=torch.int32).to(torch.uint8)
+    master = clean.clone()
+    master.scatter_(1, locs, master.gather(1, locs) ^ vals)
+    eras = locs[:, 8:].to(torch.int32).contiguous()
+    neras = torch.full((ncw,), 4, dtype=torch.int32, device="cuda")
+    work = torch.empty_like(master)
+    res = torch.empty(ncw, dtype=torch.int32, device="cuda")
+    codec.reserve(ncw)
+    e_ms, d_ms = timed_pair(lambda st: codec.encode(clean, K, stream=st),
+                            lambda st: codec.decode(work, K, eras=eras, neras=neras, result=res, stream=st),
+                            5, 1, pre=lambda: work.copy_(master))
+    if not bool((res == 12).all()) or not torch.equal(work, clean):
+        raise SystemExit("C3 extra: decode did not restore the batch")
+    out["c3"] = {"codewords": ncw, "decode_ms": round(d_ms, 4), "encode_ms": round(e_ms, 4),
+                 "frac_decode": round(ncw * DEC_BYTES / (d_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    log(f"extras: c3 {out['c3']}")
+    del clean, master, work, res, locs, vals, eras, neras
+    torch.cuda.empty_cache()
+    # host-memory pipeline (the north_star's PCIe-inclusive rate; DESIGN.md 5)
+    h = np.random.default_rng(3).integers(0, 256, (ncw, N)).astype(np.uint8)
+    hp = torch.from_numpy(h.copy()).pin_memory().numpy()
+    e2e = {}
+    for name, buf in (("pageable", h), ("pinned", hp)):
+        codec.encode_host(buf, K)
+        codec.decode_host(buf, K)
+        t1 = time.perf_counter()
+        for _ in range(3):
+            codec.encode_host(buf, K)
+            r = codec.decode_host(buf, K)
+        dt = (time.perf_counter() - t1) / 3
+        assert (r == 0).all()
+        e2e[name] = round(ncw * N / dt / 1e9, 3)
+    # decode of a pinned batch with 1 % of the rows corrupted (2 symbol errors each): those rows
+    # come back over PCIe
+    idx = np.arange(0, ncw, 100)
+    ref = hp.copy()
+    t_dec = 0.0
+    for _ in range(3):
+        hp[idx, 7] ^= 0x5A
+        hp[idx, 200] ^= 0xA5
+        t1 = time.perf_counter()
+        r = codec.decode_host(hp, K)
+        t_dec += time.perf_counter() - t1
+        assert int((r != 0).sum()) == len(idx) and np.array_equal(hp, ref)
+    e2e["pinned_decode_1pct_corrupted"] = round(ncw * N / (t_dec / 3) / 1e9, 3)
+    out["e2e_host_gbs"] = e2e
+    log(f"extras: e2e {e2e}")
+    return out
+
+
 def bench_shards(args):
     """SURVEY.md 8d C2 shard batches: S-byte shards (S = 1 KiB .. 1 MiB) in the rsencode layout
     (rsencode.C:93-163: 223-byte chunks, each followed by its 32 parity bytes, the last chunk
@@ -486,47 +659,8 @@ def bench_shards(args):
     gen = torch.Generator(device="cuda").manual_seed(0x5EED0003)
     sweep = []
     for S in (1 << 10, 1 << 14, 1 << 18, 1 << 20):
-        shards = max(1, (256 << 20) // S)
-        R = codec.shard_codewords(S)
-        enc = codec.shard_encoded_len(S)
-        buf = torch.randint(0, 256, (shards, enc), generator=gen, device="cuda",
-                            dtype=torch.int32).to(torch.uint8)
-        codec.reserve(shards * R)
-        res = torch.empty(shards * R, dtype=torch.int32, device="cuda")
-        stream = torch.cuda.current_stream()
-
-        def step(ev=None):
-            if ev:
-                ev[0].record(stream)
-            codec.encode_shards(buf, S, stream=stream)
-            if ev:
-                ev[1].record(stream)
-            codec.decode_shards(buf, S, result=res, stream=stream)
-            if ev:
-                ev[2].record(stream)
-        for _ in range(max(1, args.warmup)):
-            step()
-        torch.cuda.synchronize()
-        if int((res != 0).sum()):
-            raise SystemExit(f"shards S={S}: encoded shards did not decode clean")
-        steps = max(1, args.steps)
-        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
-        t0 = time.perf_counter()
-        for i in range(steps):
-            step(evs[i])
-        torch.cuda.synchronize()
-        dt = (time.perf_counter() - t0) / steps
-        enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / steps
-        dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / steps
-        enc_alg = shards * enc                         # data read + parity written
-        dec_alg = enc_alg + 4 * shards * R             # all read + result written
-        sweep.append({"shard_bytes": S, "shards": shards, "codewords": shards * R,
-                      "tail_len": S - (R - 1) * K, "gbs_shard_data": round(shards * S / dt / 1e9, 3),
-                      "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4),
-                      "frac_encode": round(enc_alg / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                      "frac_decode": round(dec_alg / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
+        sweep.append(shard_point(codec, S, args.steps, args.warmup, gen))
         log(f"shards S={S}: {sweep[-1]}")
-        del buf
     best = max(sweep, key=lambda r: r["gbs_shard_data"])
     print(json.dumps({"metric": "RS(255,223) shard-batch encode+decode GB/s device-resident (sweep)",
                       "value": best["gbs_shard_data"], "unit": "GB/s", "n_gpus": world,
@@ -548,6 +682,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=3.0,
                     help="seconds per CPU-baseline measurement (5 configs x 1/all threads)")
     ap.add_argument("--e2e", action="store_true", help="also time the host-memory pipeline")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the extra figures of the default N=1 C2 run (shards 1 KiB / 1 MiB, "
+                         "C2 at 4M codewords, C3 decode, host-memory rates)")
     ap.add_argument("--workload", choices=("c2", "c1", "c3", "c4", "c5", "shards"), default="c2",
                     help="c2: the headline RS(255,223) line; c1: the same for RS(255,251); c3: "
                          "RS(255,223) 8 errors + 4 erasures decode; c4: RS(65535,65503); c5: "
@@ -580,9 +717,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    local = bench_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("gloo")
 
     n, k = (255, 251) if args.workload == "c1" else (N, args.k or K)
     enc_bytes, dec_bytes = n, n + 4               # encode: k read + n-k written; decode: n read + result
@@ -625,7 +762,7 @@ def main():
     elapsed = time.perf_counter() - t0
     enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
     dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
-    elapsed = shard.max_over_ranks(elapsed, device="cuda")
+    elapsed = shard.max_over_ranks(elapsed)
 
     total_cw = ncw * world * args.steps
     value = total_cw * n / elapsed / 1e9
@@ -660,6 +797,10 @@ def main():
             e2e[name] = round(ncw * n / dt / 1e9, 3)
             log(f"host-memory ({name}) encode+decode: {e2e[name]} GB/s")
 
+    extras = None
+    if world == 1 and args.workload == "c2" and not args.k and not args.no_extras:
+        extras = c2_extras(codec, args)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baselines(args.cpu_seconds)
@@ -678,6 +819,8 @@ def main():
                 "roofline": roofline, "cpu_baseline": cpu}
         if e2e is not None:
             line["e2e_host_gbs"] = e2e
+        if extras is not None:
+            line.update(extras)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -263,21 +263,31 @@ def emit_fold_epilogue(out, gf, fname, T, nlw_expr, seq):
     out.append("}")
 
 
-def emit_weight_block(out, fname_sig, weights, B, I="    "):
+def emit_weight_block(out, fname_sig, weights, B, I="    ", first=False, opaque=False):
     """One main-loop block: positions 8B..8B+7 (X[0..7]) into state V[s][q] for the GF(2^8)
-    weight functions weights[s](p) (V[s] accumulates sum_p bit_b(x_p) weights[s](p))."""
+    weight functions weights[s](p) (V[s] accumulates sum_p bit_b(x_p) weights[s](p)).
+    first: set the state instead of accumulating (a wave's first block).  opaque: accumulate
+    through inline-asm XORs (acc_xor3 / acc_xor2), so the compiler cannot reassociate the state
+    chains across blocks (which keeps every block's combinations live to the end and spills)."""
+    xf3, xf2 = ("acc_xor3", "acc_xor2") if opaque else ("xor3", None)
     out.append(fname_sig + " {")
     emit_combos(out, "l", [f"X[{t}]" for t in range(4)], I)
     emit_combos(out, "h", [f"X[{t}]" for t in range(4, 8)], I)
+    acc, first_rows = [], []
     for s_, wf in enumerate(weights):
         for q in range(8):
             m1 = sum(((wf(8 * B + t) >> q) & 1) << t for t in range(4))
             m2 = sum(((wf(8 * B + 4 + t) >> q) & 1) << t for t in range(4))
             terms = ([f"l{m1}"] if m1 else []) + ([f"h{m2}"] if m2 else [])
             if len(terms) == 2:
-                out.append(f"{I}V[{s_}][{q}] = xor3(V[{s_}][{q}], {terms[0]}, {terms[1]});")
+                acc.append(f"V[{s_}][{q}] = {xf3}(V[{s_}][{q}], {terms[0]}, {terms[1]});")
+                first_rows.append(f"V[{s_}][{q}] = {terms[0]} ^ {terms[1]};")
             elif terms:
-                out.append(f"{I}V[{s_}][{q}] ^= {terms[0]};")
+                acc.append(f"V[{s_}][{q}] = {xf2}(V[{s_}][{q}], {terms[0]});" if opaque else f"V[{s_}][{q}] ^= {terms[0]};")
+                first_rows.append(f"V[{s_}][{q}] = {terms[0]};")
+            else:
+                first_rows.append(f"V[{s_}][{q}] = 0u;")
+    out.extend(f"{I}{x}" for x in (first_rows if first else acc))
     out.append("}")
 
 
@@ -311,9 +321,9 @@ def pt_exchange(groups_need, qn):
     return plan
 
 
-def pt_xcost(plan, qn):
+def pt_xcost(plan, qn, xcap=PT_XCAP):
     rounds = qn.bit_length() - 1
-    return sum(max(-(-len(plan[q][r][0]) // PT_XCAP) for q in range(qn)) for r in range(rounds))
+    return sum(max(-(-len(plan[q][r][0]) // xcap) for q in range(qn)) for r in range(rounds))
 
 
 class PtRole:
@@ -322,9 +332,10 @@ class PtRole:
     waves split the positions; a recursive-halving exchange leaves every wave the totals of the
     items its epilogue folds (seq = [(item slot, output index, squarings)])."""
 
-    def __init__(self, c: PsCodec, enc: bool):
+    def __init__(self, c: PsCodec, enc: bool, waves=PT_WAVES, gn=None, xcap=PT_XCAP):
         from itertools import combinations, permutations
         self.c, self.enc = c, enc
+        self.nwaves, self.xcap = waves, xcap
         gf = c.gf
         K = N - c.nr
         self.hi = K if enc else N
@@ -343,10 +354,10 @@ class PtRole:
             nitems = len(c.leaders)
             self.wfun = [(lambda p, l=l: c.w(l, p) if p < N else 0) for l in c.leaders]
             outs = [sorted(c.members[l], key=lambda x: x[1]) for l in c.leaders]
-        self.gn = max(1, -(-nitems // 8))
-        while PT_WAVES % self.gn:
+        self.gn = gn if gn else max(1, -(-nitems // 8))
+        while waves % self.gn:
             self.gn += 1
-        self.qn = PT_WAVES // self.gn
+        self.qn = waves // self.gn
         size = [len(o) for o in outs]
         # 1. items -> GN groups of (nearly) equal item and output counts; 2. per group, outputs ->
         #    QN waves by recursive halving of the group's output multiset, which is the exchange's
@@ -412,7 +423,7 @@ class PtRole:
                     used[s] = u + k
                 bins[q] = b
             plan = pt_exchange([set(s for s, _, _ in b) for b in bins], self.qn)
-            return (pt_xcost(plan, self.qn), max(-(-len(b) // 4) for b in bins),
+            return (pt_xcost(plan, self.qn, xcap), max(-(-len(b) // 4) for b in bins),
                     sum(len(x[0]) for pq in plan for x in pq)), bins, plan
 
         if self.gn == 1:
@@ -451,17 +462,17 @@ class PtRole:
                 self.waves[w] = {"g": g, "q": q, "plan": plan[q], "own": own,
                                  "seq": [(own.index(s), m, k) for s, m, k in seq]}
         self.rounds = self.qn.bit_length() - 1
-        # sub-rounds: <= PT_XCAP items per wave at a time (the exchange area)
+        # sub-rounds: <= xcap items per wave at a time (the exchange area)
         self.subs = []                                        # (round, chunk index)
         for r in range(self.rounds):
-            nch = max(-(-len(self.waves[w]["plan"][r][0]) // PT_XCAP) for w in range(PT_WAVES))
+            nch = max(-(-len(self.waves[w]["plan"][r][0]) // xcap) for w in range(waves))
             self.subs += [(r, ch) for ch in range(nch)]
         self.nown = max(1, max(len(v["own"]) for v in self.waves.values()))
         self.nq = max(1, max(-(-len(v["seq"]) // 4) for v in self.waves.values()))
         # 4. pieces (16 positions) per wave: half 0 = pieces 0..7, half 1 = 8..; round-robin
         npieces = -(-self.hi // 16)
         self.pieces = {}
-        for w in range(PT_WAVES):
+        for w in range(waves):
             q = self.waves[w]["q"]
             h0 = [p for p in range(0, min(8, npieces)) if p % self.qn == q % self.qn]
             h1 = [p for p in range(8, npieces) if (p - 8) % self.qn == q % self.qn]
@@ -520,8 +531,9 @@ def gen_pt(c: PsCodec):
            "    // syndrome index of quad slot (W, quad, j), -1 = none",
            f"    static constexpr int SYN[{W}][{R.nq}][4] = " + "{" + ", ".join(
                "{" + ", ".join(fmt_list(q) for q in syn[w]) + "}" for w in range(W)) + "};",
-           "    // positions 8B..8B+7 (words X) into group G's state (B: the absolute 8-position block)",
-           "    template <int G, int B> static __device__ void block(uint32_t (&V)[NI][8], const uint32_t (&X)[8]);",
+           "    // positions 8B..8B+7 (words X) into group G's state (B: the absolute 8-position block;",
+           "    // F: the wave's first block, which sets the state instead of accumulating into it)",
+           "    template <int G, int B, bool F> static __device__ void block(uint32_t (&V)[NI][8], const uint32_t (&X)[8]);",
            "    // group G's partials of quarter Q (computed with quarter 0's weights) times alpha^(-16 Q e)",
            "    template <int G, int Q> static __device__ void fix(uint32_t (&V)[NI][8]);",
            "    template <int W, class F> static __device__ void epilogue(const uint32_t (&T)[NOWN][8], F &&emit);",
@@ -535,8 +547,9 @@ def gen_pt(c: PsCodec):
         pall = sorted(set(p for w in range(W) if R.waves[w]["g"] == g for p in R.pieces[w][0] + R.pieces[w][1]))
         for pc in pall:
             for B in (2 * pc, 2 * pc + 1):
-                emit_weight_block(out, f"template <> __device__ __forceinline__ void {st}::block<{g}, {B}>("
-                                  "uint32_t (&V)[NI][8], const uint32_t (&X)[8])", ws, B)
+                for F in ((True, False) if B == 2 * pc else (False,)):
+                    emit_weight_block(out, f"template <> __device__ __forceinline__ void {st}::block<{g}, {B}, {str(F).lower()}>("
+                                      "uint32_t (&V)[NI][8], const uint32_t (&X)[8])", ws, B, first=F, opaque=True)
         for q in range(1, R.qn):
             out.append(f"template <> __device__ __forceinline__ void {st}::fix<{g}, {q}>(uint32_t (&V)[NI][8]) {{")
             out.append("    uint32_t t[8];")
@@ -556,6 +569,81 @@ def gen_pt(c: PsCodec):
     return "\n".join(out)
 
 
+# ---- 4-wave tile kernel (k_pq): each wave evaluates ALL leaders over its own run of positions ------
+PQ_WAVES = 4
+PQ_XCAP = 8               # items a wave sends per exchange sub-round (4 x 8 x 2 KiB = the 64 KiB image)
+PQ_CODECS = {"RS_255_223"}
+
+
+def gen_pq(c: PsCodec):
+    """PQ_<codec>: the 4-wave tile kernel's tables and straight-line code.  Wave W evaluates every
+    coset leader (NI x 8 state words) over its own contiguous run of 8-position blocks, with each
+    block's own network (no quarter fix-ups, no leader groups: reads and Four-Russians combinations
+    are done once per position); a two-round recursive-halving exchange then leaves every wave the
+    totals of the leaders whose syndromes (two quads) it folds.  Encode runs the same networks over
+    the data positions (the kernel masks positions >= K) for k_ps_parity8."""
+    out = []
+    R = PtRole(c, False, waves=PQ_WAVES, gn=1, xcap=PQ_XCAP)
+    st = f"PQ_{c.name}"
+    W = PQ_WAVES
+    X = PQ_XCAP
+    nsub = max(len(R.subs), 1)
+
+    def pad(xs, n, v=-1):
+        return list(xs) + [v] * (n - len(xs))
+    xs = [[pad(R.waves[w]["plan"][r][0][X * ch:X * ch + X], X) for (r, ch) in R.subs] or [[-1] * X]
+          for w in range(W)]
+    xv = [[pad(R.waves[w]["plan"][r][1][X * ch:X * ch + X], X) for (r, ch) in R.subs] or [[-1] * X]
+          for w in range(W)]
+    syn = [[[R.waves[w]["seq"][4 * qd + j][1] if 4 * qd + j < len(R.waves[w]["seq"]) else -1
+             for j in range(4)] for qd in range(R.nq)] for w in range(W)]
+    # 8-position blocks per direction, split into W contiguous runs (decode: all N positions;
+    # encode: the data positions)
+    runs = []
+    for hi in (N, N - c.nr):
+        nb = -(-hi // 8)
+        cut = [round(nb * w / W) for w in range(W + 1)]
+        runs.append((nb, cut))
+    hdr = [f"struct {st} {{",
+           f"    static constexpr unsigned POLY = {c.poly:#x}, FCR = {c.fcr}, PRIM = {c.prim}, NR = {c.nr};",
+           f"    static constexpr int NI = {R.ni}, NOWN = {R.nown}, NQ = {R.nq};",
+           f"    static constexpr int NSUB = {len(R.subs)}, XCAP = {X};",
+           "    // 8-position blocks of wave W: [B0[E][W], B0[E][W + 1]) (E = 0 decode, 1 encode)",
+           f"    static constexpr int NB[2] = {{{runs[0][0]}, {runs[1][0]}}};",
+           f"    static constexpr int B0[2][{W + 1}] = {{{fmt_list(runs[0][1])}, {fmt_list(runs[1][1])}}};",
+           "    // exchange sub-round s (round XR[s]): wave W sends item slots XS[W][s], adds the",
+           "    // partner's words into slots XV[W][s] (partner = W ^ (1 << XR[s]))",
+           f"    static constexpr int XR[{nsub}] = {fmt_list([r for r, _ in R.subs] or [0])};",
+           f"    static constexpr int XS[{W}][{nsub}][{X}] = " + "{" + ", ".join(
+               "{" + ", ".join(fmt_list(x) for x in xs[w]) + "}" for w in range(W)) + "};",
+           f"    static constexpr int XV[{W}][{nsub}][{X}] = " + "{" + ", ".join(
+               "{" + ", ".join(fmt_list(x) for x in xv[w]) + "}" for w in range(W)) + "};",
+           "    // item slots whose totals wave W folds (T[i] <-> slot OWN[W][i])",
+           f"    static constexpr int OWN[{W}][{R.nown}] = " + "{" + ", ".join(
+               fmt_list(pad(R.waves[w]["own"], R.nown)) for w in range(W)) + "};",
+           "    // syndrome index of quad slot (W, quad, j), -1 = none",
+           f"    static constexpr int SYN[{W}][{R.nq}][4] = " + "{" + ", ".join(
+               "{" + ", ".join(fmt_list(q) for q in syn[w]) + "}" for w in range(W)) + "};",
+           "    // positions 8B..8B+7 (words X) into every leader's state",
+           "    // F: the wave's first block (sets the state instead of accumulating into it)",
+           "    template <int B, bool F> static __device__ void block(uint32_t (&V)[NI][8], const uint32_t (&X)[8]);",
+           "    template <int W, class F> static __device__ void epilogue(const uint32_t (&T)[NOWN][8], F &&emit);",
+           "};"]
+    out += hdr
+    ws = [R.wfun[i] for i in R.groups[0]]
+    for B in range(runs[0][0]):
+        for F in (True, False):
+            emit_weight_block(out, f"template <> __device__ __forceinline__ void {st}::block<{B}, {str(F).lower()}>("
+                              "uint32_t (&V)[NI][8], const uint32_t (&X)[8])", ws, B, first=F, opaque=True)
+    for w in range(W):
+        emit_fold_epilogue(out, c.gf, f"{st}_epi{w}", "T", f"{st}::NOWN", R.waves[w]["seq"])
+    out.append(f"template <int W, class F> __device__ __forceinline__ void {st}::epilogue("
+               "const uint32_t (&T)[NOWN][8], F &&emit) {")
+    out.append("    " + " else ".join(f"if constexpr (W == {w}) {st}_epi{w}(T, emit);" for w in range(W)))
+    out.append("}")
+    return "\n".join(out)
+
+
 def main(dst=None):
     dst = dst or os.path.join(HERE, "..", "csrc", "gen", "ezrs_ps_tables.inc")
     os.makedirs(os.path.dirname(dst), exist_ok=True)
@@ -564,6 +652,17 @@ def main(dst=None):
             "#pragma once", "#include <cstdint>", "namespace ezrs { namespace ps {",
             "__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {",
             "    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);", "}",
+            "// state accumulation of the 4-wave kernel: opaque to the compiler's XOR reassociation",
+            "__device__ __forceinline__ uint32_t acc_xor3(uint32_t a, uint32_t b, uint32_t c) {",
+            "    uint32_t r;",
+            "    asm(\"v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96\" : \"=v\"(r) : \"v\"(a), \"v\"(b), \"v\"(c));",
+            "    return r;",
+            "}",
+            "__device__ __forceinline__ uint32_t acc_xor2(uint32_t a, uint32_t b) {",
+            "    uint32_t r;",
+            "    asm(\"v_xor_b32 %0, %1, %2\" : \"=v\"(r) : \"v\"(a), \"v\"(b));",
+            "    return r;",
+            "}",
             "// (m & a) | (~m & b): v_bfi_b32",
             "__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {",
             "    return (m & a) | (~m & b);", "}"]
@@ -571,7 +670,11 @@ def main(dst=None):
         c = PsCodec(*cd)
         body.append(gen_parity(c))
         body.append(gen_pt(c))
+        if c.name in PQ_CODECS:
+            body.append(gen_pq(c))
 
+    body.append("// codecs with the 4-wave tile kernel (PQ_<codec>)")
+    body.append("#define EZRS_PQ_CODEC_LIST(X) " + " ".join(f"X({cd[0]})" for cd in CODECS if cd[0] in PQ_CODECS))
     body.append("#define EZRS_PS_CODEC_LIST(X) \\")
     for i, cd in enumerate(CODECS):
         sep = " \\" if i + 1 < len(CODECS) else ""

@@ -58,8 +58,14 @@ __device__ unsigned long long g_pt_stamps[16][8][8][8];
 #define PT_STAMP(ph) do { __builtin_amdgcn_sched_barrier(0); if (blockIdx.x < 16 && pt_it < 8 && \
     __lane_id() == 0) g_pt_stamps[blockIdx.x][pt_w][pt_it][ph] = __builtin_amdgcn_s_memtime(); \
     __builtin_amdgcn_sched_barrier(0); } while (0)
+// tools/micro/pq_stamps.hip: the same for the 4-wave kernel, [wg][wave][tile][phase]
+__device__ unsigned long long g_pq_stamps[16][4][8][8];
+#define PQ_STAMP(ph) do { __builtin_amdgcn_sched_barrier(0); if (blockIdx.x < 16 && pq_it < 8 && \
+    __lane_id() == 0) g_pq_stamps[blockIdx.x][W][pq_it][ph] = __builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0); } while (0)
 #else
 #define PT_STAMP(ph) do { } while (0)
+#define PQ_STAMP(ph) do { } while (0)
 #endif
 
 struct PsArgs {
@@ -253,16 +259,25 @@ __device__ __forceinline__ void issue_tile_lin(uint32_t lbuf, pw_rsrc_t rsrc, ui
 // Positions pa .. pa+7 (words X) with the network of quarter 0's block B0; positions before lo
 // (the zero pad of a shortened code: the image holds the previous row's bytes there) and at or
 // past HI contribute nothing.  pa, lo wave-uniform.
-template <class C, int G, int HI, int B0>
-__device__ __forceinline__ void block8_rt(uint32_t (&V)[C::NI][8], uint32_t (&X)[8], int pa, int lo) {
-    const int dlo = lo - pa, dhi = HI - pa;
-    if (dhi <= 0 || dlo >= 8) return;
-    if (dlo > 0 || dhi < 8) {
+// F: the wave's first block (sets the state: never skipped, its masked positions are zeros).
+// LO0: full-length rows (lo == 0, the common case): no run-time masks, so no branches -- the
+// branches around every block cost a register shuffle each.
+template <class C, int G, int HI, int B0, int PA, bool F, bool LO0>
+__device__ __forceinline__ void block8_rt(uint32_t (&V)[C::NI][8], uint32_t (&X)[8], int lo) {
+    constexpr int dhi = HI - PA;
+    if constexpr (dhi <= 0 && !F) return;
+    if constexpr (dhi < 8) {
 #pragma unroll
         for (int t = 0; t < 8; ++t)
-            if (t < dlo || t >= dhi) X[t] = 0;
+            if (t >= dhi) X[t] = 0;
     }
-    C::template block<G, B0>(V, X);
+    if constexpr (!LO0) {
+        const int dlo = lo - PA;                             // wave-uniform
+        if (!F && dlo >= 8) return;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) X[t] = t < dlo ? 0u : X[t];
+    }
+    C::template block<G, B0, F>(V, X);
 }
 
 // Rows 4l + k, positions pa .. pa+15 (k = 0..3): R[k] = 16 bytes of row k.
@@ -333,7 +348,7 @@ __device__ __forceinline__ void read_rows_shard(u32x4 (&R)[4], uint32_t lbuf, in
 // Quarter Q's pieces.  Default: each piece runs its own networks (block index = its absolute
 // 8-position block).  EZRS_PT_SHARED_NETS (variant builds): quarter 0's networks on every quarter,
 // then fix<G, Q> multiplies the partials by alpha^(-16 Q e) (smaller code, more VALU).
-template <class C, int G, int Q, int HI, bool SH>
+template <class C, int G, int Q, int HI, bool SH, bool LO0>
 __device__ __forceinline__ void lin_pass(uint32_t (&V)[C::NI][8], uint32_t lbuf, uint32_t stride, int lo,
                                          const uint32_t (&ph)[4], int tail_lo) {
 #ifdef EZRS_PT_SHARED_NETS
@@ -342,6 +357,7 @@ __device__ __forceinline__ void lin_pass(uint32_t (&V)[C::NI][8], uint32_t lbuf,
     constexpr int BQ = Q;
 #endif
     constexpr int NP = C::NP0[G] + C::NP1[G];
+    static_assert(16 * (C::PIECE[G][0] + Q) < HI, "the wave's first block sets its state");
     u32x4 e = {0, 0, 0, 0};
     if constexpr (SH)
         asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(e) : "v"(lbuf + kTab + 16u * fresh()) : "memory");
@@ -361,14 +377,14 @@ __device__ __forceinline__ void lin_pass(uint32_t (&V)[C::NI][8], uint32_t lbuf,
                     transpose4x4(c0, X);
                     transpose4x4(c1, X + 4);
                 }
-                block8_rt<C, G, HI, 2 * (p0 + BQ)>(V, X, pa, lo);
+                block8_rt<C, G, HI, 2 * (p0 + BQ), pa, I == 0, LO0>(V, X, lo);
                 {
                     const uint32_t c2[4] = {R[0].z, R[1].z, R[2].z, R[3].z};
                     const uint32_t c3[4] = {R[0].w, R[1].w, R[2].w, R[3].w};
                     transpose4x4(c2, X);
                     transpose4x4(c3, X + 4);
                 }
-                block8_rt<C, G, HI, 2 * (p0 + BQ) + 1>(V, X, pa + 8, lo);
+                block8_rt<C, G, HI, 2 * (p0 + BQ) + 1, pa + 8, false, LO0>(V, X, lo);
             }
         }
     });
@@ -469,7 +485,7 @@ __device__ __forceinline__ void wave_tail_lin(uint32_t (&V)[C::NI][8], const PsA
     PT_STAMP(6);
 }
 
-template <class C, bool ENC, int W, bool SH>
+template <class C, bool ENC, int W, bool SH, bool LO0>
 __device__ __forceinline__ void pt_run_lin(const PsArgs &a, uint8_t *lds) {
     constexpr int G = W % C::GN, Q = W / C::GN;
     const int w = W;
@@ -506,11 +522,7 @@ __device__ __forceinline__ void pt_run_lin(const PsArgs &a, uint8_t *lds) {
         for (int k = 0; k < 4; ++k) ph[k] = (lbuf + kGuard + k * a.stride - (uint32_t)lo) & 3u;
         uint32_t nbytes = 0;
         const uint32_t noff = tile + gridDim.x < a.ntiles ? tile_range(tile + gridDim.x, nbytes) : kOob;
-        uint32_t V[C::NI][8];
-#pragma unroll
-        for (int s = 0; s < C::NI; ++s)
-#pragma unroll
-            for (int t = 0; t < 8; ++t) V[s][t] = 0;
+        uint32_t V[C::NI][8];                                // set by the wave's first block
         PT_STAMP(0);
         wait_vm<0>();                                        // the tile landed (and the stores went)
         if constexpr (SH) {                                  // row table: wave w writes rows 32w ..
@@ -552,7 +564,7 @@ __device__ __forceinline__ void pt_run_lin(const PsArgs &a, uint8_t *lds) {
             const uint32_t t0 = tile * kTile, kt = (t0 / a.srows) * a.srows + a.srows - 1;
             if (kt < t0 + kTile && kt < a.ncw) tlo = a.stail_lo;
         }
-        if (!(a.ablate & 1)) lin_pass<C, G, Q, HI, SH>(V, lbuf, a.stride, lo, ph, tlo);
+        lin_pass<C, G, Q, HI, SH, LO0>(V, lbuf, a.stride, lo, ph, tlo);
 #if EZRS_PT_PRIO
         asm volatile("s_setprio 0");
 #endif
@@ -566,7 +578,7 @@ __device__ __forceinline__ void pt_run_lin(const PsArgs &a, uint8_t *lds) {
     wait_vm<0>();                                            // no DMA may land after the exit
 }
 
-template <class C, bool ENC, bool SH>
+template <class C, bool ENC, bool SH, bool LO0>
 __global__ void __attribute__((amdgpu_flat_work_group_size(kThreads, kThreads), amdgpu_waves_per_eu(4)))
 k_pt_lin(PsArgs a) {
     static_assert(C::NQ == 1, "one quad (4 syndromes) per wave");
@@ -575,18 +587,414 @@ k_pt_lin(PsArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLds];
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     switch (w) {                                             // each wave's pieces and tail, compiled
-    case 0: pt_run_lin<C, ENC, 0, SH>(a, lds); break;
-    case 1: pt_run_lin<C, ENC, 1, SH>(a, lds); break;
-    case 2: pt_run_lin<C, ENC, 2, SH>(a, lds); break;
-    case 3: pt_run_lin<C, ENC, 3, SH>(a, lds); break;
-    case 4: pt_run_lin<C, ENC, 4, SH>(a, lds); break;
-    case 5: pt_run_lin<C, ENC, 5, SH>(a, lds); break;
-    case 6: pt_run_lin<C, ENC, 6, SH>(a, lds); break;
-    default: pt_run_lin<C, ENC, 7, SH>(a, lds); break;
+    case 0: pt_run_lin<C, ENC, 0, SH, LO0>(a, lds); break;
+    case 1: pt_run_lin<C, ENC, 1, SH, LO0>(a, lds); break;
+    case 2: pt_run_lin<C, ENC, 2, SH, LO0>(a, lds); break;
+    case 3: pt_run_lin<C, ENC, 3, SH, LO0>(a, lds); break;
+    case 4: pt_run_lin<C, ENC, 4, SH, LO0>(a, lds); break;
+    case 5: pt_run_lin<C, ENC, 5, SH, LO0>(a, lds); break;
+    case 6: pt_run_lin<C, ENC, 6, SH, LO0>(a, lds); break;
+    default: pt_run_lin<C, ENC, 7, SH, LO0>(a, lds); break;
     }
 }
 
 } // namespace pt
+
+// ---- 4-wave tile kernel k_pq_lin (PQ_<codec>, codegen gen_pq) -----------------------------------
+// One 256-thread workgroup (4 waves) per 256-codeword tile, two workgroups per CU (80 KiB LDS
+// each), up to 256 VGPRs (2 waves per SIMD).  Wave W evaluates EVERY coset leader (NI x 8 state
+// words) over its own contiguous run of 8-position blocks with each block's own network: the
+// tile's rows are read and their Four-Russians combinations formed once (the 8-wave kernel reads
+// every position twice, once per leader group, and fixes up three quarters by alpha^(-16 q e)).
+// The next piece's LDS reads are in flight while the current piece's networks run.  Then a
+// two-round recursive-halving exchange through the consumed image leaves each wave the totals of
+// the leaders whose two quads of syndromes it folds.  Image, DMA, flags and stores as k_pt_lin.
+namespace pq {
+
+using pt::kGuard;
+using pt::kImage;
+using pt::kOob;
+using pt::u32x2;
+using pt::u32x4;
+constexpr int kThreads = 256;
+constexpr int kWaves = 4;
+constexpr int kLds = 81920;                   // 80 KiB: two workgroups per CU
+constexpr int kFlags = kGuard + kImage;       // decode flags [4][64] after the image
+constexpr int kTab = kFlags + 1024;           // shard batches: per-row image offset and pad [256]
+static_assert(kTab + 1024 <= kLds, "pq tile kernel LDS");
+
+// Raw dwords of rows 4l + k at one 16-position piece (4-byte aligned reads, aligned afterwards).
+struct Raw {
+    u32x2 e[4][2];
+    uint32_t d4[4];
+};
+
+// the piece at byte offset OFF (a multiple of 8) from the rows' dword-aligned position-0 addresses
+// at4[k]: the offset rides in the instructions' immediates
+template <int OFF>
+__device__ __forceinline__ void issue_at(Raw &r, const uint32_t (&at4)[4]) {
+    static_assert(OFF % 4 == 0 && OFF / 4 + 4 < 256, "ds_read2 dword offsets");
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        asm volatile("ds_read2_b32 %0, %3 offset0:%4 offset1:%5\n\t"
+                     "ds_read2_b32 %1, %3 offset0:%6 offset1:%7\n\t"
+                     "ds_read_b32 %2, %3 offset:%8"
+                     : "=&v"(r.e[k][0]), "=&v"(r.e[k][1]), "=&v"(r.d4[k])
+                     : "v"(at4[k]), "n"(OFF / 4), "n"(OFF / 4 + 1), "n"(OFF / 4 + 2), "n"(OFF / 4 + 3), "n"(OFF + 16)
+                     : "memory");
+}
+__device__ __forceinline__ void wait_raw(Raw &r) {
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(r.e[0][0]), "+v"(r.e[0][1]), "+v"(r.d4[0]), "+v"(r.e[1][0]), "+v"(r.e[1][1]), "+v"(r.d4[1]),
+                   "+v"(r.e[2][0]), "+v"(r.e[2][1]), "+v"(r.d4[2]), "+v"(r.e[3][0]), "+v"(r.e[3][1]), "+v"(r.d4[3])
+                 :: "memory");
+}
+// byte address of row 4l + k at position 0 (plain batches: packed rows of pitch `stride`, the
+// first byte at position lo; shard batches: the row-table entry e[k] = image offset of position 0 |
+// pad << 24)
+template <bool SH>
+__device__ __forceinline__ void row_addrs(uint32_t (&at)[4], uint32_t lbuf, uint32_t stride, int lo, const u32x4 &e) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if constexpr (SH) at[k] = lbuf + (e[k] & 0xFFFFFFu);
+        else at[k] = lbuf + kGuard + (4u * pt::fresh() + k) * stride - (uint32_t)lo;
+    }
+}
+// aligned 16 bytes of each row; shard batches: bytes before a shortened row's own pad masked off
+template <bool SH>
+__device__ __forceinline__ void align_rows(u32x4 (&R)[4], const Raw &r, const uint32_t (&at)[4], int pa,
+                                          int tail_lo, const u32x4 &e) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t d[5] = {r.e[k][0].x, r.e[k][0].y, r.e[k][1].x, r.e[k][1].y, r.d4[k]};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) R[k][j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], at[k]);
+    }
+    if constexpr (SH) {
+        if (pa < tail_lo) {                                  // wave-uniform
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int z8 = 8 * ((int)(e[k] >> 24) - pa);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int c = min(max(z8 - 32 * j, 0), 32);
+                    R[k][j] &= (uint32_t)(0xFFFFFFFFull << c);
+                }
+            }
+        }
+    }
+}
+
+// block B (positions 8B .. 8B+7, words X) into every leader (F: the wave's first block sets the
+// state); positions at/after HI contribute nothing, nor -- unless LO0 (full-length rows, the common
+// case, compiled without the run-time masks and their branches) -- positions before lo
+template <class C, int HI, int B, bool F, bool LO0>
+__device__ __forceinline__ void block8(uint32_t (&V)[C::NI][8], uint32_t (&X)[8], int lo) {
+    constexpr int pa = 8 * B;
+    if constexpr (pa >= HI) return;
+    if constexpr (HI - pa < 8) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+            if (t >= HI - pa) X[t] = 0;
+    }
+    if constexpr (!LO0) {
+        const int dlo = lo - pa;                             // wave-uniform
+#pragma unroll
+        for (int t = 0; t < 8; ++t) X[t] = t < dlo ? 0u : X[t];
+    }
+    C::template block<B, F>(V, X);
+}
+
+// Piece I of wave W (blocks B and B+1 from the run's start, 16 positions): wait for its reads,
+// issue the next piece's, run its networks.
+template <class C, bool ENC, int W, bool SH, bool LO0, int I>
+__device__ __forceinline__ void piece(uint32_t (&V)[C::NI][8], Raw &cur, const uint32_t (&at)[4],
+                                      const uint32_t (&at4)[4], int lo, int tail_lo, const u32x4 &e) {
+    constexpr int E = ENC ? 1 : 0;
+    constexpr int HI = ENC ? kN - (int)C::NR : kN;
+    constexpr int b0 = C::B0[E][W], b1 = C::B0[E][W + 1];
+    constexpr int B = b0 + 2 * I;
+    if constexpr (B < b1) {
+        wait_raw(cur);
+        Raw nxt;
+#ifndef EZRS_PQ_NOPREFETCH
+        if constexpr (B + 2 < b1) issue_at<8 * (B + 2)>(nxt, at4);
+#endif
+        __builtin_amdgcn_sched_barrier(0);
+        u32x4 R[4];
+        align_rows<SH>(R, cur, at, 8 * B, tail_lo, e);
+        uint32_t X[8];
+        {
+            const uint32_t c0[4] = {R[0].x, R[1].x, R[2].x, R[3].x};
+            const uint32_t c1[4] = {R[0].y, R[1].y, R[2].y, R[3].y};
+            transpose4x4(c0, X);
+            transpose4x4(c1, X + 4);
+        }
+        block8<C, HI, B, I == 0, LO0>(V, X, lo);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (B + 1 < b1) {
+            const uint32_t c2[4] = {R[0].z, R[1].z, R[2].z, R[3].z};
+            const uint32_t c3[4] = {R[0].w, R[1].w, R[2].w, R[3].w};
+            transpose4x4(c2, X);
+            transpose4x4(c3, X + 4);
+            block8<C, HI, B + 1, false, LO0>(V, X, lo);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#ifdef EZRS_PQ_NOPREFETCH
+        if constexpr (B + 2 < b1) issue_at<8 * (B + 2)>(nxt, at4);
+#endif
+        if constexpr (B + 2 < b1) piece<C, ENC, W, SH, LO0, I + 1>(V, nxt, at, at4, lo, tail_lo, e);
+    }
+}
+
+template <class C, bool ENC, int W, bool SH, bool LO0>
+__device__ __forceinline__ void pq_pass(uint32_t (&V)[C::NI][8], uint32_t lbuf, uint32_t stride, int lo,
+                                        int tail_lo) {
+    constexpr int E = ENC ? 1 : 0;
+    constexpr int b0 = C::B0[E][W];
+    u32x4 e = {0, 0, 0, 0};
+    if constexpr (SH)
+        asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(e) : "v"(lbuf + kTab + 16u * pt::fresh()) : "memory");
+    Raw cur;
+    uint32_t at[4], at4[4];
+    row_addrs<SH>(at, lbuf, stride, lo, e);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) at4[k] = at[k] & ~3u;        // byte phase at[k] & 3 for v_alignbyte
+    issue_at<8 * b0>(cur, at4);
+    piece<C, ENC, W, SH, LO0, 0>(V, cur, at, at4, lo, tail_lo, e);
+}
+
+// Recursive-halving exchange (partner W ^ (1 << XR[s])), slots of XCAP items x 2 KiB per wave.
+template <class C, int W, int S, int J = 0>
+__device__ __forceinline__ void xsend(uint32_t (&V)[C::NI][8], uint32_t lx) {
+    if constexpr (J < C::XCAP) {
+        constexpr int it = C::XS[W][S][J];
+        if constexpr (it >= 0) {
+            const u32x4 w0 = {V[it][0], V[it][1], V[it][2], V[it][3]};
+            const u32x4 w1 = {V[it][4], V[it][5], V[it][6], V[it][7]};
+            asm volatile("ds_write_b128 %0, %1 offset:%3\n\t"
+                         "ds_write_b128 %0, %2 offset:%4"
+                         :: "v"(lx + W * C::XCAP * 2048u), "v"(w0), "v"(w1), "n"(J * 2048),
+                            "n"(J * 2048 + 1024) : "memory");
+        }
+        xsend<C, W, S, J + 1>(V, lx);
+    }
+}
+template <class C, int W, int S, int J = 0>
+__device__ __forceinline__ void xrecv(uint32_t (&V)[C::NI][8], uint32_t lx) {
+    if constexpr (J < C::XCAP) {
+        constexpr int it = C::XV[W][S][J];
+        constexpr int PW = W ^ (1 << C::XR[S]);
+        if constexpr (it >= 0) {
+            u32x4 w0, w1;
+            asm volatile("ds_read_b128 %0, %2 offset:%3\n\t"
+                         "ds_read_b128 %1, %2 offset:%4\n\t"
+                         "s_waitcnt lgkmcnt(0)"
+                         : "=&v"(w0), "=&v"(w1) : "v"(lx + PW * C::XCAP * 2048u), "n"(J * 2048),
+                           "n"(J * 2048 + 1024) : "memory");
+            V[it][0] ^= w0.x; V[it][1] ^= w0.y; V[it][2] ^= w0.z; V[it][3] ^= w0.w;
+            V[it][4] ^= w1.x; V[it][5] ^= w1.y; V[it][6] ^= w1.z; V[it][7] ^= w1.w;
+        }
+        xrecv<C, W, S, J + 1>(V, lx);
+    }
+}
+template <class C, int W, int S>
+__device__ __forceinline__ void exchange(uint32_t (&V)[C::NI][8], uint32_t lx) {
+    if constexpr (S < C::NSUB) {
+        xsend<C, W, S>(V, lx);
+        pt::wait_lgkm();
+        pt::barrier();
+        xrecv<C, W, S>(V, lx);
+        pt::barrier();                                       // read before the area is reused
+        exchange<C, W, S + 1>(V, lx);
+    }
+}
+
+__device__ __forceinline__ void issue_tile(uint32_t lbuf, pw_rsrc_t rsrc, uint32_t toff, uint32_t tile_bytes, int w) {
+#ifdef EZRS_PQ_ABL_NODMA
+    return;                                                  // timing-only builds (pq_stamps)
+#endif
+    const uint32_t ninstr = (tile_bytes + 1023) >> 10;
+    const uint32_t lo16 = 16u * pt::fresh();
+    for (uint32_t i = w; i < ninstr; i += kWaves)
+        asm volatile("s_mov_b32 m0, %0\n\t"
+                     "s_nop 0\n\t"
+                     "buffer_load_dwordx4 %1, %2, 0 offen lds"
+                     :: "s"(lbuf + kGuard + i * 1024u), "v"(toff + i * 1024u + lo16), "s"(rsrc) : "memory", "m0");
+}
+
+// Exchange, next tile's DMA, fold and stores of wave W.
+template <class C, bool ENC, int W>
+__device__ __forceinline__ void wave_tail(uint32_t (&V)[C::NI][8], const PsArgs &a, uint32_t lbuf, uint32_t tile,
+                                          uint32_t noff, uint32_t nbytes, pw_rsrc_t rsrc, pw_rsrc_t rout,
+                                          pw_rsrc_t rws, int pq_it = 0) {
+    (void)pq_it;
+    exchange<C, W, 0>(V, lbuf + 16u * pt::fresh());
+    PQ_STAMP(4);
+    if (noff != kOob) issue_tile(lbuf, rsrc, noff, nbytes, W);
+    uint32_t T[C::NOWN][8];
+#pragma unroll
+    for (int i = 0; i < C::NOWN; ++i)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) T[i][t] = C::OWN[W][i] >= 0 ? V[C::OWN[W][i] < 0 ? 0 : C::OWN[W][i]][t] : 0u;
+    uint32_t Qs[C::NQ][8], nz = 0;
+    C::template epilogue<W>(T, [&](auto qc, uint32_t (&Qw)[8]) {
+        constexpr int qd = decltype(qc)::value;
+        constexpr uint32_t vm = (C::SYN[W][qd][0] >= 0 ? 0x01010101u : 0u) | (C::SYN[W][qd][1] >= 0 ? 0x02020202u : 0u) |
+                                (C::SYN[W][qd][2] >= 0 ? 0x04040404u : 0u) | (C::SYN[W][qd][3] >= 0 ? 0x08080808u : 0u);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            nz |= Qw[t] & vm;
+            Qs[qd][t] = Qw[t];
+        }
+    });
+    PQ_STAMP(5);
+    const uint32_t cw0 = tile * kTile + 4u * pt::fresh();    // byte k <-> codeword cw0 + k
+    if constexpr (ENC) {
+        static_for<0, C::NQ>([&](auto qc) {
+            constexpr int qd = decltype(qc)::value;
+            transpose8(Qs[qd]);                              // Qs[qd][jj] byte k: syndrome jj, codeword k
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj)
+                if (C::SYN[W][qd][jj] >= 0)
+                    pt::store_dword(rws, (uint32_t)(C::SYN[W][qd][jj] * a.ws_pitch) + cw0, Qs[qd][jj]);
+        });
+    } else {
+        uint32_t fl = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (nz >> (8 * k) & 0xFF) fl |= 1u << k;
+        const uint32_t fa = lbuf + kFlags + 256u * W + 4u * pt::fresh();
+        asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" :: "v"(fa), "v"(fl) : "memory");
+        pt::barrier();
+        {
+            uint32_t f[4];
+            const uint32_t fb = lbuf + kFlags + 4u * pt::fresh();
+            asm volatile("ds_read_b32 %0, %4\n\t"
+                         "ds_read_b32 %1, %4 offset:256\n\t"
+                         "ds_read_b32 %2, %4 offset:512\n\t"
+                         "ds_read_b32 %3, %4 offset:768\n\t"
+                         "s_waitcnt lgkmcnt(0)"
+                         : "=&v"(f[0]), "=&v"(f[1]), "=&v"(f[2]), "=&v"(f[3]) : "v"(fb) : "memory");
+            fl = f[0] | f[1] | f[2] | f[3];
+        }
+        if constexpr (W == 0) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                pt::store_dword(rout, (cw0 + k) * 4u, (fl >> k & 1) ? (uint32_t)kSentinel : 0u);
+        }
+        if (__ballot(fl != 0) != 0) {                        // flagged codewords: their syndromes
+            static_for<0, C::NQ>([&](auto qc) {
+                constexpr int qd = decltype(qc)::value;
+                transpose8(Qs[qd]);
+                if (a.ws_pitch == 0) {
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj)
+                        if (C::SYN[W][qd][jj] >= 0)
+                            pt::store_dword(rws, tile * (uint32_t)kSynTile + 256u * C::SYN[W][qd][jj] + 4u * pt::fresh(),
+                                            Qs[qd][jj]);
+                } else {                                     // a launch not starting a tile (shards)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const uint32_t g = (uint32_t)a.ws_pitch + cw0 + k;
+                        const uint32_t row = (fl >> k & 1) ? (g >> 8) * (uint32_t)kSynTile + (g & 255u) : kOob;
+#pragma unroll
+                        for (int jj = 0; jj < 4; ++jj)
+                            if (C::SYN[W][qd][jj] >= 0)
+                                pt::store_byte(rws, row + 256u * C::SYN[W][qd][jj], Qs[qd][jj] >> (8 * k));
+                    }
+                }
+            });
+        }
+    }
+}
+
+template <class C, bool ENC, int W, bool SH, bool LO0>
+__device__ __forceinline__ void pq_run(const PsArgs &a, uint8_t *lds) {
+    const pw_rsrc_t rsrc = pw_rsrc(a.base, a.span);
+    const uint32_t lbuf = __builtin_amdgcn_readfirstlane(lds_addr(lds));
+    const pw_rsrc_t rout = pw_rsrc(reinterpret_cast<const uint8_t *>(a.result), ENC ? 0u : a.ncw * 4u);
+    const pw_rsrc_t rws = pw_rsrc(a.ws, ENC ? (uint32_t)(C::NR * a.ws_pitch)
+                                            : (uint32_t)((a.ws_pitch + a.ncw + 255) / 256 * kSynTile));
+    auto tile_range = [&](uint32_t t, uint32_t &bytes) -> uint32_t {
+        if (!SH) {
+            bytes = a.stride * kTile;
+            return t * bytes;
+        }
+        int lo;
+        const uint32_t t0 = t * kTile, off = pt::row_at(a, t0, lo);
+        bytes = (t0 + kTile < a.ncw ? pt::row_at(a, t0 + kTile, lo) : a.span) - off;
+        return off;
+    };
+    uint32_t tile = blockIdx.x;
+    uint32_t tbytes, toff = tile < a.ntiles ? tile_range(tile, tbytes) : 0u;
+    if (tile < a.ntiles) issue_tile(lbuf, rsrc, toff, tbytes, W);
+    int pq_it = 0;
+    (void)pq_it;
+    for (; tile < a.ntiles; tile += gridDim.x, ++pq_it) {
+        PQ_STAMP(0);
+        int lo = a.lo;
+        asm volatile("" : "+s"(lo));
+        uint32_t nbytes = 0;
+        const uint32_t noff = tile + gridDim.x < a.ntiles ? tile_range(tile + gridDim.x, nbytes) : kOob;
+        uint32_t V[C::NI][8];                                // set by the wave's first block
+        pt::wait_vm<0>();                                    // the tile landed (and the stores went)
+        if constexpr (SH) {                                  // row table: wave W writes rows 64W ..
+            const uint32_t r = 64u * (uint32_t)W + pt::fresh(), k = tile * kTile + r;
+            uint32_t e = kGuard;
+            if (k < a.ncw) {
+                int rlo;
+                const uint32_t at = pt::row_at(a, k, rlo);
+                e = (kGuard + at - toff - (uint32_t)rlo) | ((uint32_t)rlo << 24);
+            }
+            asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" :: "v"(lbuf + kTab + 4u * r), "v"(e) : "memory");
+        }
+        pt::barrier();
+        if (toff + tbytes >= a.span) {                       // last tile: the span's final bytes
+            if (W == 0) {
+                const uint32_t off = a.span - 64u + pt::fresh();
+                uint32_t v;
+                asm volatile("buffer_load_ubyte %0, %1, %2, 0 offen\n\ts_waitcnt vmcnt(0)"
+                             : "=&v"(v) : "v"(off), "s"(rsrc) : "memory");
+                if (off >= toff && off < a.span)
+                    asm volatile("ds_write_b8 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                                 :: "v"(lbuf + kGuard + (off - toff)), "v"(v) : "memory");
+            }
+            pt::barrier();
+        }
+        int tlo = lo;                                        // shard batches: pad of the tile's rows
+        if constexpr (SH) {
+            const uint32_t t0 = tile * kTile, kt = (t0 / a.srows) * a.srows + a.srows - 1;
+            if (kt < t0 + kTile && kt < a.ncw) tlo = a.stail_lo;
+        }
+        PQ_STAMP(1);
+        pq_pass<C, ENC, W, SH, LO0>(V, lbuf, a.stride, lo, tlo);
+        PQ_STAMP(2);
+        pt::barrier();                                       // the image is consumed
+        PQ_STAMP(3);
+        wave_tail<C, ENC, W>(V, a, lbuf, tile, noff, nbytes, rsrc, rout, rws, pq_it);
+        PQ_STAMP(6);
+        toff = noff;
+        tbytes = nbytes;
+    }
+    pt::wait_vm<0>();                                        // no DMA may land after the exit
+}
+
+template <class C, bool ENC, bool SH, bool LO0>
+__global__ void __attribute__((amdgpu_flat_work_group_size(kThreads, kThreads), amdgpu_waves_per_eu(2)))
+k_pq_lin(PsArgs a) {
+    static_assert(kWaves * C::XCAP * 2048 <= kGuard + kImage, "exchange area");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kLds];
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    switch (w) {
+    case 0: pq_run<C, ENC, 0, SH, LO0>(a, lds); break;
+    case 1: pq_run<C, ENC, 1, SH, LO0>(a, lds); break;
+    case 2: pq_run<C, ENC, 2, SH, LO0>(a, lds); break;
+    default: pq_run<C, ENC, 3, SH, LO0>(a, lds); break;
+    }
+}
+
+} // namespace pq
 
 // ---- encode, stage 2: parity = V^-1 S on 32-codeword bit-sliced registers -------------------
 // Syndromes (encode workspace) -> parity rows.
@@ -701,6 +1109,44 @@ unsigned syn_grid(const DevCodec &d, uint32_t ntiles) {
 
 } // namespace
 
+// Codecs with the 4-wave tile kernel (PQ_<codec>; codegen PQ_CODECS) use it for both directions
+// (r04f: C2 1161 vs 1062 GB/s on k_pt_lin); the others, and variant builds with -DEZRS_NO_PQ (A/B
+// timing, tools/build_variant.sh), run the 8-wave k_pt_lin.
+template <class PS> struct PqFor { using type = void; };
+#define EZRS_PQ_FOR(C) template <> struct PqFor<ps::PS_##C> { using type = ps::PQ_##C; };
+EZRS_PQ_CODEC_LIST(EZRS_PQ_FOR)
+#undef EZRS_PQ_FOR
+
+template <class PS, class PT, bool ENC>
+void launch_tile(const ps::PsArgs &p, bool shard, unsigned grid, hipStream_t s) {
+    using PQ = typename PqFor<PS>::type;
+#ifndef EZRS_NO_PQ
+    if constexpr (!std::is_void<PQ>::value) {
+        const bool lo0 = p.lo == 0;                          // full-length rows: no pad masks
+        if (shard && lo0)
+            hipLaunchKernelGGL((ps::pq::k_pq_lin<PQ, ENC, true, true>), dim3(grid), dim3(ps::pq::kThreads), 0, s, p);
+        else if (shard)
+            hipLaunchKernelGGL((ps::pq::k_pq_lin<PQ, ENC, true, false>), dim3(grid), dim3(ps::pq::kThreads), 0, s, p);
+        else if (lo0)
+            hipLaunchKernelGGL((ps::pq::k_pq_lin<PQ, ENC, false, true>), dim3(grid), dim3(ps::pq::kThreads), 0, s, p);
+        else
+            hipLaunchKernelGGL((ps::pq::k_pq_lin<PQ, ENC, false, false>), dim3(grid), dim3(ps::pq::kThreads), 0, s, p);
+        return;
+    }
+#endif
+#ifndef EZRS_PQ_ONLY                                          // (ISA inspection builds: tools/pq_isa.sh)
+    const bool lo0 = p.lo == 0;                              // full-length rows: no pad masks
+    if (shard && lo0)
+        hipLaunchKernelGGL((ps::pt::k_pt_lin<PT, ENC, true, true>), dim3(grid), dim3(ps::pt::kThreads), 0, s, p);
+    else if (shard)
+        hipLaunchKernelGGL((ps::pt::k_pt_lin<PT, ENC, true, false>), dim3(grid), dim3(ps::pt::kThreads), 0, s, p);
+    else if (lo0)
+        hipLaunchKernelGGL((ps::pt::k_pt_lin<PT, ENC, false, true>), dim3(grid), dim3(ps::pt::kThreads), 0, s, p);
+    else
+        hipLaunchKernelGGL((ps::pt::k_pt_lin<PT, ENC, false, false>), dim3(grid), dim3(ps::pt::kThreads), 0, s, p);
+#endif
+}
+
 int planeslice_codec_id(const DevCodec &d) {
     int id = 0, found = -1;
 #define EZRS_PS_MATCH(C) \
@@ -802,12 +1248,7 @@ hipError_t launch_ps_encode(int id, const DevCodec &d, const EncodeArgs &a, void
 #define EZRS_PS_ENC(C)                                                                            \
         if (k++ == id) {                                                                          \
             const unsigned pgrid = (unsigned)((n + ps::kParCw - 1) / ps::kParCw);                 \
-            if (a.sh.rows)                                                                        \
-                hipLaunchKernelGGL((ps::pt::k_pt_lin<ps::PT_##C, true, true>), dim3(grid),        \
-                                   dim3(ps::pt::kThreads), 0, s, p);                              \
-            else                                                                                  \
-                hipLaunchKernelGGL((ps::pt::k_pt_lin<ps::PT_##C, true, false>), dim3(grid),       \
-                                   dim3(ps::pt::kThreads), 0, s, p);                              \
+            launch_tile<ps::PS_##C, ps::PT_##C, true>(p, a.sh.rows != 0, grid, s);                \
             hipLaunchKernelGGL((ps::k_ps_parity8<ps::PS_##C>), dim3(pgrid), dim3(512), 0, s,      \
                                static_cast<const uint8_t *>(ws), p.ws_pitch, par, a.parity_stride, n, \
                                a.sh, a.len);                                                      \
@@ -847,14 +1288,7 @@ hipError_t launch_ps_syndromes(int id, const DevCodec &d, const DecodeArgs &a, u
         const unsigned grid = syn_grid(d, p.ntiles);
         int k = 0;
 #define EZRS_PS_SYN(C)                                                                            \
-        if (k++ == id) {                                                                          \
-            if (a.sh.rows)                                                                        \
-                hipLaunchKernelGGL((ps::pt::k_pt_lin<ps::PT_##C, false, true>), dim3(grid),       \
-                                   dim3(ps::pt::kThreads), 0, s, p);                              \
-            else                                                                                  \
-                hipLaunchKernelGGL((ps::pt::k_pt_lin<ps::PT_##C, false, false>), dim3(grid),      \
-                                   dim3(ps::pt::kThreads), 0, s, p);                              \
-        }
+        if (k++ == id) launch_tile<ps::PS_##C, ps::PT_##C, false>(p, a.sh.rows != 0, grid, s);
         EZRS_PS_CODEC_LIST(EZRS_PS_SYN)
 #undef EZRS_PS_SYN
         hipError_t e = hipGetLastError();

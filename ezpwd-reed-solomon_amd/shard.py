@@ -24,7 +24,9 @@ def _group_ready():
 
 
 def max_over_ranks(x: float, device=None) -> float:
-    """The largest x over all ranks (the timing rule of bench.py); x itself without a group."""
+    """The largest x over all ranks (the timing rule of bench.py); x itself without a group.
+    bench.py's group is gloo (CPU): the scalars never touch a device, so ranks can even share one
+    GPU (tests/test_bench_gpu.py runs --gpus 2 on a one-GPU box)."""
     if not _group_ready():
         return float(x)
     import torch
