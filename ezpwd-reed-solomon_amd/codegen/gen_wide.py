@@ -255,9 +255,9 @@ def gen_codec(m, poly, fcr, prim, nr):
     return tag, out
 
 
-def main():
+def main(dst=None):
     here = os.path.dirname(os.path.abspath(__file__))
-    dst = os.path.join(here, "..", "csrc", "gen", "ezrs_wide_tables.inc")
+    dst = dst or os.path.join(here, "..", "csrc", "gen", "ezrs_wide_tables.inc")
     body = ["// Generated by codegen/gen_wide.py -- do not edit.",
             "#pragma once",
             "namespace ezrs {",
@@ -281,4 +281,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(next((a for a in sys.argv[1:] if a != "-v"), None))

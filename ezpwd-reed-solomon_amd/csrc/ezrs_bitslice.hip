@@ -28,8 +28,8 @@
 //
 // Decode (k_bs_syndromes): codewords whose syndromes are all zero (and carry no erasures) get
 // result 0 -- exactly what decode_symbols returns (rs_base:1416-1434); all others get a sentinel
-// and their syndromes go to the workspace for the error-path kernel (ezrs_generic.hip:
-// k_decode_flagged), which runs the reference's BM/Chien/Forney on them.
+// and their syndromes go to the workspace for the error-path kernel (ezrs_errors.hip:
+// k_decode_errors), which runs the reference's BM/Chien/Forney on them.
 // Encode: k_bs_encode_syn computes the syndromes of the data words into a workspace of bit-planes
 // of 32-codeword groups; k_bs_parity maps them to parity with the GF(2) map Q (generated) on full
 // 32-slot registers and stores each codeword's parity bytes.

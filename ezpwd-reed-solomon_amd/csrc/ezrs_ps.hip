@@ -198,23 +198,56 @@ __device__ __forceinline__ void xsend(uint32_t (&V)[C::NI][8], uint32_t lx) {
         xsend<C, W, S, J + 1>(V, lx);
     }
 }
-template <class C, int W, int S, int J = 0>
-__device__ __forceinline__ void xrecv(uint32_t (&V)[C::NI][8], uint32_t lx) {
+// Add the partner PW's items of sub-round S (XV) into V, the reads two items ahead of the XORs:
+// LDS latency is paid once per sub-round, not once per item.
+template <class C, int W, int S>
+constexpr int xnext(int j) {
+    ++j;
+    while (j < C::XCAP && C::XV[W][S][j] < 0) ++j;
+    return j;
+}
+template <class C, int PW, int J>
+__device__ __forceinline__ void xread(u32x4 (&b)[2], uint32_t lx) {
+    asm volatile("ds_read_b128 %0, %2 offset:%3\n\t"
+                 "ds_read_b128 %1, %2 offset:%4"
+                 : "=&v"(b[0]), "=&v"(b[1]) : "v"(lx + PW * C::XCAP * 2048u), "n"(J * 2048), "n"(J * 2048 + 1024)
+                 : "memory");
+}
+template <int N>
+__device__ __forceinline__ void xwait(u32x4 (&b)[2]) {
+    asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(b[0]), "+v"(b[1]) : "n"(N) : "memory");
+}
+// cur = item J and nx = item xnext(J) are in flight
+template <class C, int W, int S, int PW, int J>
+__device__ __forceinline__ void xrecv_run(uint32_t (&V)[C::NI][8], uint32_t lx, u32x4 (&cur)[2], u32x4 (&nx)[2]) {
     if constexpr (J < C::XCAP) {
-        constexpr int it = C::XV[W][S][J];
-        constexpr int PW = W ^ (C::GN << C::XR[S]);
-        if constexpr (it >= 0) {
-            u32x4 w0, w1;
-            asm volatile("ds_read_b128 %0, %2 offset:%3\n\t"
-                         "ds_read_b128 %1, %2 offset:%4\n\t"
-                         "s_waitcnt lgkmcnt(0)"
-                         : "=&v"(w0), "=&v"(w1) : "v"(lx + PW * C::XCAP * 2048u), "n"(J * 2048),
-                           "n"(J * 2048 + 1024) : "memory");
-            V[it][0] ^= w0.x; V[it][1] ^= w0.y; V[it][2] ^= w0.z; V[it][3] ^= w0.w;
-            V[it][4] ^= w1.x; V[it][5] ^= w1.y; V[it][6] ^= w1.z; V[it][7] ^= w1.w;
+        constexpr int J1 = xnext<C, W, S>(J), J2 = xnext<C, W, S>(J1);
+        u32x4 nn[2];
+        if constexpr (J2 < C::XCAP) {
+            xread<C, PW, J2>(nn, lx);
+            xwait<4>(cur);
+        } else if constexpr (J1 < C::XCAP) {
+            xwait<2>(cur);
+        } else {
+            xwait<0>(cur);
         }
-        xrecv<C, W, S, J + 1>(V, lx);
+        constexpr int it = C::XV[W][S][J];
+        V[it][0] ^= cur[0].x; V[it][1] ^= cur[0].y; V[it][2] ^= cur[0].z; V[it][3] ^= cur[0].w;
+        V[it][4] ^= cur[1].x; V[it][5] ^= cur[1].y; V[it][6] ^= cur[1].z; V[it][7] ^= cur[1].w;
+        xrecv_run<C, W, S, PW, J1>(V, lx, nx, nn);
     }
+}
+template <class C, int W, int S, int PW>
+__device__ __forceinline__ void xrecv_pipe(uint32_t (&V)[C::NI][8], uint32_t lx) {
+    constexpr int J0 = xnext<C, W, S>(-1), J1 = xnext<C, W, S>(J0);
+    u32x4 a[2], b[2];
+    if constexpr (J0 < C::XCAP) xread<C, PW, J0>(a, lx);
+    if constexpr (J1 < C::XCAP) xread<C, PW, J1>(b, lx);
+    xrecv_run<C, W, S, PW, J0>(V, lx, a, b);
+}
+template <class C, int W, int S>
+__device__ __forceinline__ void xrecv(uint32_t (&V)[C::NI][8], uint32_t lx) {
+    xrecv_pipe<C, W, S, W ^ (C::GN << C::XR[S])>(V, lx);
 }
 template <class C, int W, int S>
 __device__ __forceinline__ void exchange(uint32_t (&V)[C::NI][8], uint32_t lx) {
@@ -780,23 +813,9 @@ __device__ __forceinline__ void xsend(uint32_t (&V)[C::NI][8], uint32_t lx) {
         xsend<C, W, S, J + 1>(V, lx);
     }
 }
-template <class C, int W, int S, int J = 0>
+template <class C, int W, int S>
 __device__ __forceinline__ void xrecv(uint32_t (&V)[C::NI][8], uint32_t lx) {
-    if constexpr (J < C::XCAP) {
-        constexpr int it = C::XV[W][S][J];
-        constexpr int PW = W ^ (1 << C::XR[S]);
-        if constexpr (it >= 0) {
-            u32x4 w0, w1;
-            asm volatile("ds_read_b128 %0, %2 offset:%3\n\t"
-                         "ds_read_b128 %1, %2 offset:%4\n\t"
-                         "s_waitcnt lgkmcnt(0)"
-                         : "=&v"(w0), "=&v"(w1) : "v"(lx + PW * C::XCAP * 2048u), "n"(J * 2048),
-                           "n"(J * 2048 + 1024) : "memory");
-            V[it][0] ^= w0.x; V[it][1] ^= w0.y; V[it][2] ^= w0.z; V[it][3] ^= w0.w;
-            V[it][4] ^= w1.x; V[it][5] ^= w1.y; V[it][6] ^= w1.z; V[it][7] ^= w1.w;
-        }
-        xrecv<C, W, S, J + 1>(V, lx);
-    }
+    pt::xrecv_pipe<C, W, S, W ^ (1 << C::XR[S])>(V, lx);
 }
 template <class C, int W, int S>
 __device__ __forceinline__ void exchange(uint32_t (&V)[C::NI][8], uint32_t lx) {
