@@ -63,9 +63,14 @@ __device__ unsigned long long g_pq_stamps[16][4][8][8];
 #define PQ_STAMP(ph) do { __builtin_amdgcn_sched_barrier(0); if (blockIdx.x < 16 && pq_it < 8 && \
     __lane_id() == 0) g_pq_stamps[blockIdx.x][W][pq_it][ph] = __builtin_amdgcn_s_memtime(); \
     __builtin_amdgcn_sched_barrier(0); } while (0)
+// tools/micro/par_stamps.hip: the parity kernel's phases, [block][wave][phase]
+__device__ unsigned long long g_par_stamps[64][8][8];
+#define PAR_STAMP(ph) do { __builtin_amdgcn_sched_barrier(0); if (blockIdx.x < 64 && __lane_id() == 0) \
+    g_par_stamps[blockIdx.x][wave][ph] = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
 #else
 #define PT_STAMP(ph) do { } while (0)
 #define PQ_STAMP(ph) do { } while (0)
+#define PAR_STAMP(ph) do { } while (0)
 #endif
 
 struct PsArgs {
@@ -850,7 +855,9 @@ __device__ __forceinline__ void wave_tail(uint32_t (&V)[C::NI][8], const PsArgs 
     (void)pq_it;
     exchange<C, W, 0>(V, lbuf + 16u * pt::fresh());
     PQ_STAMP(4);
+#ifndef EZRS_PQ_DMA_LATE
     if (noff != kOob) issue_tile(lbuf, rsrc, noff, nbytes, W);
+#endif
     uint32_t T[C::NOWN][8];
 #pragma unroll
     for (int i = 0; i < C::NOWN; ++i)
@@ -868,6 +875,9 @@ __device__ __forceinline__ void wave_tail(uint32_t (&V)[C::NI][8], const PsArgs 
         }
     });
     PQ_STAMP(5);
+#ifdef EZRS_PQ_DMA_LATE
+    if (noff != kOob) issue_tile(lbuf, rsrc, noff, nbytes, W);
+#endif
     const uint32_t cw0 = tile * kTile + 4u * pt::fresh();    // byte k <-> codeword cw0 + k
     if constexpr (ENC) {
         static_for<0, C::NQ>([&](auto qc) {
@@ -987,7 +997,13 @@ __device__ __forceinline__ void pq_run(const PsArgs &a, uint8_t *lds) {
             if (kt < t0 + kTile && kt < a.ncw) tlo = a.stail_lo;
         }
         PQ_STAMP(1);
+#ifdef EZRS_PQ_PRIO
+        asm volatile("s_setprio 1");
+#endif
         pq_pass<C, ENC, W, SH, LO0>(V, lbuf, a.stride, lo, tlo);
+#ifdef EZRS_PQ_PRIO
+        asm volatile("s_setprio 0");
+#endif
         PQ_STAMP(2);
         pt::barrier();                                       // the image is consumed
         PQ_STAMP(3);
@@ -1041,15 +1057,30 @@ __global__ void __launch_bounds__(512) k_ps_parity8(const uint8_t *ws, size_t ws
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const size_t g0 = (size_t)blockIdx.x * kParGroups;
     const uint8_t *src = ws + (g0 + lane) * 32;                // ws rows are padded to 2048 cw
-    for (int i = wave; i < NR; i += 8) {
-        const uint4 v0 = *reinterpret_cast<const uint4 *>(src + i * ws_pitch);
-        const uint4 v1 = *reinterpret_cast<const uint4 *>(src + i * ws_pitch + 16);
-        uint32_t D[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-        transpose8(D);                                         // D[q] bit 8k + m: cw 4m + k
+    PAR_STAMP(0);
+    constexpr int NRW = (NR + 7) / 8;                          // syndromes per wave
+    uint4 v[NRW][2];
 #pragma unroll
-        for (int qq = 0; qq < 8; ++qq) lds[(8 * i + qq) * 64 + lane] = D[qq];
+    for (int r = 0; r < NRW; ++r) {                            // every load in flight at once
+        const int i = wave + 8 * r;
+        if (i < NR) {
+            v[r][0] = *reinterpret_cast<const uint4 *>(src + i * ws_pitch);
+            v[r][1] = *reinterpret_cast<const uint4 *>(src + i * ws_pitch + 16);
+        }
     }
+#pragma unroll
+    for (int r = 0; r < NRW; ++r) {
+        const int i = wave + 8 * r;
+        if (i < NR) {
+            uint32_t D[8] = {v[r][0].x, v[r][0].y, v[r][0].z, v[r][0].w, v[r][1].x, v[r][1].y, v[r][1].z, v[r][1].w};
+            transpose8(D);                                     // D[q] bit 8k + m: cw 4m + k
+#pragma unroll
+            for (int qq = 0; qq < 8; ++qq) lds[(8 * i + qq) * 64 + lane] = D[qq];
+        }
+    }
+    PAR_STAMP(1);
     __syncthreads();
+    PAR_STAMP(2);
     uint32_t O[4][8];
     switch (wave) {
     case 0: C::template q_pass4<0>(O, lds + lane, 64); break;
@@ -1061,7 +1092,9 @@ __global__ void __launch_bounds__(512) k_ps_parity8(const uint8_t *ws, size_t ws
     case 6: if constexpr (C::NPASS4 > 6) C::template q_pass4<6>(O, lds + lane, 64); break;
     default: if constexpr (C::NPASS4 > 7) C::template q_pass4<7>(O, lds + lane, 64); break;
     }
+    PAR_STAMP(3);
     __syncthreads();                                           // planes consumed
+    PAR_STAMP(4);
     uint8_t *stage = reinterpret_cast<uint8_t *>(lds);
     if (wave < C::NPASS4) {
         const int nj = NR - 4 * wave < 4 ? NR - 4 * wave : 4;
@@ -1081,7 +1114,9 @@ __global__ void __launch_bounds__(512) k_ps_parity8(const uint8_t *ws, size_t ws
                 }
             }
     }
+    PAR_STAMP(5);
     __syncthreads();
+    PAR_STAMP(6);
     const size_t cwb = g0 * 32;
     for (int r = threadIdx.x; r < kParCw; r += 512) {
         const size_t x = cwb + r;
@@ -1107,6 +1142,7 @@ __global__ void __launch_bounds__(512) k_ps_parity8(const uint8_t *ws, size_t ws
             for (int o = 0; o < NR; ++o) dst[o] = s8[o];
         }
     }
+    PAR_STAMP(7);
 }
 
 } // namespace ps
