@@ -145,21 +145,29 @@ def mat_apply(out, dst, src, rows, ind, extra=None):
 
 def gen_parity(c: PsCodec):
     """PS_<codec>: the codec's constants and the parity map passes over 32-codeword bit-sliced
-    syndromes, q_pass4<P> = parity symbols 4P .. 4P+3 (k_ps_parity8, wave P)."""
+    syndromes, q_pass4<P> = parity symbols 4P .. 4P+3 (k_ps_parity8, wave P).  The planes of
+    syndromes 8c .. 8c+7 arrive as chunk c: before its first read of chunk c >= 1 a pass calls
+    ready(std::integral_constant<int, c>) (k_ps_parity8 stages its loads by chunk)."""
     st = f"PS_{c.name}"
+    npass = (c.nr + 3) // 4
     out = [f"struct {st} {{",
            f"    static constexpr unsigned POLY = {c.poly:#x}, FCR = {c.fcr}, PRIM = {c.prim}, NR = {c.nr};",
-           "    template <int P> static __device__ void q_pass4(uint32_t (&O)[4][8], const uint32_t *in, int ld);",
-           f"    static constexpr int NPASS4 = {(c.nr + 3) // 4};",
-           "};"]
+           f"    static constexpr int NPASS4 = {npass};"]
+    out += [f"    template <class R> static __device__ void q4_{P}(uint32_t (&O)[4][8], const uint32_t *in, int ld, "
+            "R &&ready);" for P in range(npass)]
+    out.append("    template <int P, class R> static __device__ __forceinline__ void q_pass4(uint32_t (&O)[4][8], "
+               "const uint32_t *in, int ld, R &&ready) {")
+    out.append("        " + " else ".join(f"if constexpr (P == {P}) q4_{P}(O, in, ld, ready);" for P in range(npass)))
+    out.append("    }")
+    out.append("};")
     I = "    "
     Q = c.q_rows()
     nr = c.nr
     PW = 4
-    for P in range((nr + PW - 1) // PW):
+    for P in range(npass):
         j0, nj = PW * P, min(PW, nr - PW * P)
-        out.append(f"template <> __device__ __forceinline__ void {st}::q_pass4<{P}>("
-                   f"uint32_t (&O)[{PW}][8], const uint32_t *in, int ld) {{")
+        out.append(f"template <class R> __device__ __forceinline__ void {st}::q4_{P}("
+                   f"uint32_t (&O)[{PW}][8], const uint32_t *in, int ld, R &&ready) {{")
         first = [[True] * 8 for _ in range(nj)]
         out.append(f"{I}uint32_t N[8];")
         out.append(f"{I}#pragma unroll")
@@ -170,6 +178,8 @@ def gen_parity(c: PsCodec):
             out.append(f"{I}    #pragma unroll")
             out.append(f"{I}    for (int q = 0; q < 8; ++q) P[q] = N[q];")
             if i + 1 < nr:
+                if (i + 1) % 8 == 0:
+                    out.append(f"{I}    ready(std::integral_constant<int, {(i + 1) // 8}>{{}});")
                 out.append(f"{I}    #pragma unroll")
                 out.append(f"{I}    for (int q = 0; q < 8; ++q) N[q] = in[({8 * (i + 1)} + q) * ld];")
             out.append(f"{I}    __builtin_amdgcn_sched_barrier(0);")
@@ -186,9 +196,9 @@ def gen_parity(c: PsCodec):
                         out.append(f"{I}    {dst} = " + (" ^ ".join(terms) if terms else "0u") + ";")
                         first[jl][b] = False
                     elif len(terms) == 2:
-                        out.append(f"{I}    {dst} = xor3({dst}, {terms[0]}, {terms[1]});")
+                        out.append(f"{I}    {dst} = acc_xor3({dst}, {terms[0]}, {terms[1]});")
                     elif terms:
-                        out.append(f"{I}    {dst} ^= {terms[0]};")
+                        out.append(f"{I}    {dst} = acc_xor2({dst}, {terms[0]});")
             out.append(f"{I}    __builtin_amdgcn_sched_barrier(0);")
             out.append(f"{I}}}")
         out.append("}")
@@ -213,12 +223,20 @@ def emit_fold_epilogue(out, gf, fname, T, nlw_expr, seq):
     a2 = lin_rows(lambda x: gf.mul(4, x))
     a4 = lin_rows(lambda x: gf.mul(16, x))
 
-    def fold_level(dst, src, rows, sh, ind):
+    def fold_level(dst, src, rows, sh, ind, up=False):
+        """dst = src + alpha^k (src one step up), at the lower bit positions of each pair of
+        positions sh apart -- or, up, at the upper ones (src shifted up instead), so that the
+        next pack needs no shift."""
         out.append(f"{ind}{{")
         out.append(f"{ind}    uint32_t y[8];")
-        out.append(f"{ind}    for (int b = 0; b < 8; ++b) y[b] = {src}[b] >> {sh};")
-        mat_apply(out, [f"{dst}[{q}]" for q in range(8)], [f"y[{b}]" for b in range(8)], rows, ind + "    ",
-                  extra=[f"{src}[{q}]" for q in range(8)])
+        if up:
+            out.append(f"{ind}    for (int b = 0; b < 8; ++b) y[b] = {src}[b] << {sh};")
+            mat_apply(out, [f"{dst}[{q}]" for q in range(8)], [f"{src}[{b}]" for b in range(8)], rows,
+                      ind + "    ", extra=[f"y[{q}]" for q in range(8)])
+        else:
+            out.append(f"{ind}    for (int b = 0; b < 8; ++b) y[b] = {src}[b] >> {sh};")
+            mat_apply(out, [f"{dst}[{q}]" for q in range(8)], [f"y[{b}]" for b in range(8)], rows,
+                      ind + "    ", extra=[f"{src}[{q}]" for q in range(8)])
         out.append(f"{ind}}}")
 
     out.append(f"template <class F> __device__ __forceinline__ void {fname}("
@@ -247,16 +265,16 @@ def emit_fold_epilogue(out, gf, fname, T, nlw_expr, seq):
         for j in range(4):
             out.append(f"{I}    uint32_t F{j}[8];")
             if j < len(part):
-                fold_level(f"F{j}", srcs[j], a1, 1, I + "    ")
+                fold_level(f"F{j}", srcs[j], a1, 1, I + "    ", up=j % 2 == 1)
             else:
                 out.append(f"{I}    for (int b = 0; b < 8; ++b) F{j}[b] = 0u;")
         for pj in range(2):
             out.append(f"{I}    uint32_t P{pj}[8], G{pj}[8];")
             out.append(f"{I}    for (int b = 0; b < 8; ++b) P{pj}[b] = bfi(0x55555555u, "
-                       f"F{2 * pj}[b], F{2 * pj + 1}[b] << 1);")
-            fold_level(f"G{pj}", f"P{pj}", a2, 2, I + "    ")
+                       f"F{2 * pj}[b], F{2 * pj + 1}[b]);")
+            fold_level(f"G{pj}", f"P{pj}", a2, 2, I + "    ", up=pj == 1)
         out.append(f"{I}    uint32_t H[8], Q[8];")
-        out.append(f"{I}    for (int b = 0; b < 8; ++b) H[b] = bfi(0x33333333u, G0[b], G1[b] << 2);")
+        out.append(f"{I}    for (int b = 0; b < 8; ++b) H[b] = bfi(0x33333333u, G0[b], G1[b]);")
         fold_level("Q", "H", a4, 4, I + "    ")
         out.append(f"{I}    emit(std::integral_constant<int, {qd}>{{}}, Q);")
         out.append(f"{I}}}")

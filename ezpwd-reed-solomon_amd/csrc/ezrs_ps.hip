@@ -840,11 +840,32 @@ __device__ __forceinline__ void issue_tile(uint32_t lbuf, pw_rsrc_t rsrc, uint32
 #endif
     const uint32_t ninstr = (tile_bytes + 1023) >> 10;
     const uint32_t lo16 = 16u * pt::fresh();
+#ifdef EZRS_PQ_DMA_M0X4
+    // wave w: pieces 16w .. 16w+15, four per M0 value (the instruction offset steps both the
+    // source and the LDS destination)
+    for (uint32_t i = 16u * (uint32_t)w; i < 16u * (uint32_t)w + 16u && i < ninstr; i += 4) {
+        if (i + 4 <= ninstr)
+            asm volatile("s_mov_b32 m0, %0\n\t"
+                         "s_nop 0\n\t"
+                         "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+                         "buffer_load_dwordx4 %1, %2, 0 offen offset:1024 lds\n\t"
+                         "buffer_load_dwordx4 %1, %2, 0 offen offset:2048 lds\n\t"
+                         "buffer_load_dwordx4 %1, %2, 0 offen offset:3072 lds"
+                         :: "s"(lbuf + kGuard + i * 1024u), "v"(toff + i * 1024u + lo16), "s"(rsrc) : "memory", "m0");
+        else
+            for (uint32_t j = i; j < ninstr; ++j)
+                asm volatile("s_mov_b32 m0, %0\n\t"
+                             "s_nop 0\n\t"
+                             "buffer_load_dwordx4 %1, %2, 0 offen lds"
+                             :: "s"(lbuf + kGuard + j * 1024u), "v"(toff + j * 1024u + lo16), "s"(rsrc) : "memory", "m0");
+    }
+#else
     for (uint32_t i = w; i < ninstr; i += kWaves)
         asm volatile("s_mov_b32 m0, %0\n\t"
                      "s_nop 0\n\t"
                      "buffer_load_dwordx4 %1, %2, 0 offen lds"
                      :: "s"(lbuf + kGuard + i * 1024u), "v"(toff + i * 1024u + lo16), "s"(rsrc) : "memory", "m0");
+#endif
 }
 
 // Exchange, next tile's DMA, fold and stores of wave W.
@@ -1058,40 +1079,48 @@ __global__ void __launch_bounds__(512) k_ps_parity8(const uint8_t *ws, size_t ws
     const size_t g0 = (size_t)blockIdx.x * kParGroups;
     const uint8_t *src = ws + (g0 + lane) * 32;                // ws rows are padded to 2048 cw
     PAR_STAMP(0);
-    constexpr int NRW = (NR + 7) / 8;                          // syndromes per wave
-    uint4 v[NRW][2];
+    // wave w loads syndromes w + 8c (chunk c) -- every load in flight at once -- and makes chunk
+    // c's planes visible when the passes reach it, so the map runs while later chunks arrive
+    constexpr int NCH = (NR + 7) / 8;
+    pt::u32x4 v[NCH][2];
 #pragma unroll
-    for (int r = 0; r < NRW; ++r) {                            // every load in flight at once
-        const int i = wave + 8 * r;
-        if (i < NR) {
-            v[r][0] = *reinterpret_cast<const uint4 *>(src + i * ws_pitch);
-            v[r][1] = *reinterpret_cast<const uint4 *>(src + i * ws_pitch + 16);
-        }
+    for (int c = 0; c < NCH; ++c) {
+        const int i = wave + 8 * c;
+        if (i < NR)
+            asm volatile("global_load_dwordx4 %0, %2, off\n\t"
+                         "global_load_dwordx4 %1, %2, off offset:16"
+                         : "=&v"(v[c][0]), "=&v"(v[c][1]) : "v"(src + i * ws_pitch) : "memory");
     }
-#pragma unroll
-    for (int r = 0; r < NRW; ++r) {
-        const int i = wave + 8 * r;
+    auto ready = [&](auto cc) {
+        constexpr int c = decltype(cc)::value;
+        const int i = wave + 8 * c;
         if (i < NR) {
-            uint32_t D[8] = {v[r][0].x, v[r][0].y, v[r][0].z, v[r][0].w, v[r][1].x, v[r][1].y, v[r][1].z, v[r][1].w};
+            pt::u32x4 a0 = v[c][0], a1 = v[c][1];              // this chunk's two loads landed
+            asm volatile("s_waitcnt vmcnt(%2)" : "+v"(a0), "+v"(a1) : "n"(2 * (NCH - 1 - c)) : "memory");
+            uint32_t D[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
             transpose8(D);                                     // D[q] bit 8k + m: cw 4m + k
 #pragma unroll
             for (int qq = 0; qq < 8; ++qq) lds[(8 * i + qq) * 64 + lane] = D[qq];
         }
-    }
+        pt::wait_lgkm();                                       // raw barrier: later chunks' loads stay in flight
+        pt::barrier();
+    };
+    ready(std::integral_constant<int, 0>{});
     PAR_STAMP(1);
-    __syncthreads();
     PAR_STAMP(2);
     uint32_t O[4][8];
     switch (wave) {
-    case 0: C::template q_pass4<0>(O, lds + lane, 64); break;
-    case 1: if constexpr (C::NPASS4 > 1) C::template q_pass4<1>(O, lds + lane, 64); break;
-    case 2: if constexpr (C::NPASS4 > 2) C::template q_pass4<2>(O, lds + lane, 64); break;
-    case 3: if constexpr (C::NPASS4 > 3) C::template q_pass4<3>(O, lds + lane, 64); break;
-    case 4: if constexpr (C::NPASS4 > 4) C::template q_pass4<4>(O, lds + lane, 64); break;
-    case 5: if constexpr (C::NPASS4 > 5) C::template q_pass4<5>(O, lds + lane, 64); break;
-    case 6: if constexpr (C::NPASS4 > 6) C::template q_pass4<6>(O, lds + lane, 64); break;
-    default: if constexpr (C::NPASS4 > 7) C::template q_pass4<7>(O, lds + lane, 64); break;
+    case 0: C::template q_pass4<0>(O, lds + lane, 64, ready); break;
+    case 1: if constexpr (C::NPASS4 > 1) C::template q_pass4<1>(O, lds + lane, 64, ready); break;
+    case 2: if constexpr (C::NPASS4 > 2) C::template q_pass4<2>(O, lds + lane, 64, ready); break;
+    case 3: if constexpr (C::NPASS4 > 3) C::template q_pass4<3>(O, lds + lane, 64, ready); break;
+    case 4: if constexpr (C::NPASS4 > 4) C::template q_pass4<4>(O, lds + lane, 64, ready); break;
+    case 5: if constexpr (C::NPASS4 > 5) C::template q_pass4<5>(O, lds + lane, 64, ready); break;
+    case 6: if constexpr (C::NPASS4 > 6) C::template q_pass4<6>(O, lds + lane, 64, ready); break;
+    default: if constexpr (C::NPASS4 > 7) C::template q_pass4<7>(O, lds + lane, 64, ready); break;
     }
+    if (wave >= C::NPASS4)                                     // no pass: still takes every barrier
+        static_for<1, NCH>([&](auto cc) { ready(cc); });
     PAR_STAMP(3);
     __syncthreads();                                           // planes consumed
     PAR_STAMP(4);
