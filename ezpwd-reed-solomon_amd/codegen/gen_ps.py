@@ -239,8 +239,8 @@ def emit_fold_epilogue(out, gf, fname, T, nlw_expr, seq):
                       ind + "    ", extra=[f"{src}[{q}]" for q in range(8)])
         out.append(f"{ind}}}")
 
-    out.append(f"template <class F> __device__ __forceinline__ void {fname}("
-               f"const uint32_t (&{T})[{nlw_expr}][8], F &&emit) {{")
+    out.append(f"template <class F, class HK> __device__ __forceinline__ void {fname}("
+               f"const uint32_t (&{T})[{nlw_expr}][8], F &&emit, HK &&hook) {{")
     prev = {}
 
     def expand(li, m, k, ind):
@@ -268,6 +268,7 @@ def emit_fold_epilogue(out, gf, fname, T, nlw_expr, seq):
                 fold_level(f"F{j}", srcs[j], a1, 1, I + "    ", up=j % 2 == 1)
             else:
                 out.append(f"{I}    for (int b = 0; b < 8; ++b) F{j}[b] = 0u;")
+            out.append(f"{I}    hook(std::integral_constant<int, {4 * qd + j}>{{}});   // other work may go here")
         for pj in range(2):
             out.append(f"{I}    uint32_t P{pj}[8], G{pj}[8];")
             out.append(f"{I}    for (int b = 0; b < 8; ++b) P{pj}[b] = bfi(0x55555555u, "
@@ -554,7 +555,8 @@ def gen_pt(c: PsCodec):
            "    template <int G, int B, bool F> static __device__ void block(uint32_t (&V)[NI][8], const uint32_t (&X)[8]);",
            "    // group G's partials of quarter Q (computed with quarter 0's weights) times alpha^(-16 Q e)",
            "    template <int G, int Q> static __device__ void fix(uint32_t (&V)[NI][8]);",
-           "    template <int W, class F> static __device__ void epilogue(const uint32_t (&T)[NOWN][8], F &&emit);",
+           "    template <int W, class F, class H> static __device__ void epilogue(const uint32_t (&T)[NOWN][8], F &&emit, "
+           "H &&hook);",
            "};"]
     out += hdr
     gf = c.gf
@@ -580,9 +582,9 @@ def gen_pt(c: PsCodec):
             out.append("}")
     for w in range(W):
         emit_fold_epilogue(out, c.gf, f"{st}_epi{w}", "T", f"{st}::NOWN", R.waves[w]["seq"])
-    out.append(f"template <int W, class F> __device__ __forceinline__ void {st}::epilogue("
-               "const uint32_t (&T)[NOWN][8], F &&emit) {")
-    out.append("    " + " else ".join(f"if constexpr (W == {w}) {st}_epi{w}(T, emit);" for w in range(W)))
+    out.append(f"template <int W, class F, class H> __device__ __forceinline__ void {st}::epilogue("
+               "const uint32_t (&T)[NOWN][8], F &&emit, H &&hook) {")
+    out.append("    " + " else ".join(f"if constexpr (W == {w}) {st}_epi{w}(T, emit, hook);" for w in range(W)))
     out.append("}")
     return "\n".join(out)
 
@@ -645,7 +647,8 @@ def gen_pq(c: PsCodec):
            "    // positions 8B..8B+7 (words X) into every leader's state",
            "    // F: the wave's first block (sets the state instead of accumulating into it)",
            "    template <int B, bool F> static __device__ void block(uint32_t (&V)[NI][8], const uint32_t (&X)[8]);",
-           "    template <int W, class F> static __device__ void epilogue(const uint32_t (&T)[NOWN][8], F &&emit);",
+           "    template <int W, class F, class H> static __device__ void epilogue(const uint32_t (&T)[NOWN][8], F &&emit, "
+           "H &&hook);",
            "};"]
     out += hdr
     ws = [R.wfun[i] for i in R.groups[0]]
@@ -655,9 +658,9 @@ def gen_pq(c: PsCodec):
                               "uint32_t (&V)[NI][8], const uint32_t (&X)[8])", ws, B, first=F, opaque=True)
     for w in range(W):
         emit_fold_epilogue(out, c.gf, f"{st}_epi{w}", "T", f"{st}::NOWN", R.waves[w]["seq"])
-    out.append(f"template <int W, class F> __device__ __forceinline__ void {st}::epilogue("
-               "const uint32_t (&T)[NOWN][8], F &&emit) {")
-    out.append("    " + " else ".join(f"if constexpr (W == {w}) {st}_epi{w}(T, emit);" for w in range(W)))
+    out.append(f"template <int W, class F, class H> __device__ __forceinline__ void {st}::epilogue("
+               "const uint32_t (&T)[NOWN][8], F &&emit, H &&hook) {")
+    out.append("    " + " else ".join(f"if constexpr (W == {w}) {st}_epi{w}(T, emit, hook);" for w in range(W)))
     out.append("}")
     return "\n".join(out)
 

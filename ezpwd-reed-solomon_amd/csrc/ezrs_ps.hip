@@ -459,7 +459,7 @@ __device__ __forceinline__ void wave_tail_lin(uint32_t (&V)[C::NI][8], const PsA
                 nz |= Qw[t] & vm;
                 Qs[t] = Qw[t];
             }
-        });
+        }, [](auto) {});
     PT_STAMP(5);
     const uint32_t cw0 = tile * kTile + 4u * fresh();        // byte k <-> codeword cw0 + k
     if constexpr (ENC) {
@@ -868,6 +868,31 @@ __device__ __forceinline__ void issue_tile(uint32_t lbuf, pw_rsrc_t rsrc, uint32
 #endif
 }
 
+#ifdef EZRS_PQ_DMA_SPREAD
+// Group g (0..3) of wave w's pieces 16w + 4g .. 16w + 4g + 3, four per M0 value (the instruction
+// offset steps both the source and the LDS destination), issued between fold steps.
+__device__ __forceinline__ void issue_group(uint32_t lbuf, pw_rsrc_t rsrc, uint32_t toff, uint32_t tile_bytes, int w,
+                                            int g) {
+    const uint32_t ninstr = (tile_bytes + 1023) >> 10;
+    const uint32_t lo16 = 16u * pt::fresh();
+    const uint32_t i = 16u * (uint32_t)w + 4u * (uint32_t)g;
+    if (i + 4 <= ninstr)
+        asm volatile("s_mov_b32 m0, %0\n\t"
+                     "s_nop 0\n\t"
+                     "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+                     "buffer_load_dwordx4 %1, %2, 0 offen offset:1024 lds\n\t"
+                     "buffer_load_dwordx4 %1, %2, 0 offen offset:2048 lds\n\t"
+                     "buffer_load_dwordx4 %1, %2, 0 offen offset:3072 lds"
+                     :: "s"(lbuf + kGuard + i * 1024u), "v"(toff + i * 1024u + lo16), "s"(rsrc) : "memory", "m0");
+    else
+        for (uint32_t j = i; j < ninstr && j < i + 4; ++j)
+            asm volatile("s_mov_b32 m0, %0\n\t"
+                         "s_nop 0\n\t"
+                         "buffer_load_dwordx4 %1, %2, 0 offen lds"
+                         :: "s"(lbuf + kGuard + j * 1024u), "v"(toff + j * 1024u + lo16), "s"(rsrc) : "memory", "m0");
+}
+#endif
+
 // Exchange, next tile's DMA, fold and stores of wave W.
 template <class C, bool ENC, int W>
 __device__ __forceinline__ void wave_tail(uint32_t (&V)[C::NI][8], const PsArgs &a, uint32_t lbuf, uint32_t tile,
@@ -876,7 +901,7 @@ __device__ __forceinline__ void wave_tail(uint32_t (&V)[C::NI][8], const PsArgs 
     (void)pq_it;
     exchange<C, W, 0>(V, lbuf + 16u * pt::fresh());
     PQ_STAMP(4);
-#ifndef EZRS_PQ_DMA_LATE
+#if !defined(EZRS_PQ_DMA_LATE) && !defined(EZRS_PQ_DMA_SPREAD)
     if (noff != kOob) issue_tile(lbuf, rsrc, noff, nbytes, W);
 #endif
     uint32_t T[C::NOWN][8];
@@ -894,6 +919,14 @@ __device__ __forceinline__ void wave_tail(uint32_t (&V)[C::NI][8], const PsArgs 
             nz |= Qw[t] & vm;
             Qs[qd][t] = Qw[t];
         }
+    }, [&](auto pc) {
+#ifdef EZRS_PQ_DMA_SPREAD
+        constexpr int pt_ = decltype(pc)::value;             // DMA groups at fold points 1, 3, 5, 7
+        if constexpr (pt_ % 2 == 1 && pt_ < 8)
+            if (noff != kOob) issue_group(lbuf, rsrc, noff, nbytes, W, pt_ / 2);
+#else
+        (void)pc;
+#endif
     });
     PQ_STAMP(5);
 #ifdef EZRS_PQ_DMA_LATE
@@ -1085,18 +1118,19 @@ __global__ void __launch_bounds__(512) k_ps_parity8(const uint8_t *ws, size_t ws
     pt::u32x4 v[NCH][2];
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-        const int i = wave + 8 * c;
-        if (i < NR)
+        const int i = wave + 8 * c < NR ? wave + 8 * c : 0;   // past NR: a dummy load keeps the
+        {                                                      // per-chunk vmcnt counts uniform
             asm volatile("global_load_dwordx4 %0, %2, off\n\t"
                          "global_load_dwordx4 %1, %2, off offset:16"
                          : "=&v"(v[c][0]), "=&v"(v[c][1]) : "v"(src + i * ws_pitch) : "memory");
+        }
     }
     auto ready = [&](auto cc) {
         constexpr int c = decltype(cc)::value;
         const int i = wave + 8 * c;
-        if (i < NR) {
-            pt::u32x4 a0 = v[c][0], a1 = v[c][1];              // this chunk's two loads landed
-            asm volatile("s_waitcnt vmcnt(%2)" : "+v"(a0), "+v"(a1) : "n"(2 * (NCH - 1 - c)) : "memory");
+        pt::u32x4 a0 = v[c][0], a1 = v[c][1];                  // this chunk's two loads landed (the
+        asm volatile("s_waitcnt vmcnt(%2)" : "+v"(a0), "+v"(a1) : "n"(2 * (NCH - 1 - c)) : "memory");
+        if (i < NR) {                                          // registers stay live until then)
             uint32_t D[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
             transpose8(D);                                     // D[q] bit 8k + m: cw 4m + k
 #pragma unroll

@@ -14,7 +14,7 @@ timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke(); print('smok
 rc=$?; tail -n 1 $OUT/smoke.log; [ $rc -eq 0 ] || exit $rc
 for v in $VARS; do
   EZRS_LIB_VARIANT=$GRAFT_REPO_ROOT/tools/variants/libezrs_$v.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py \
-      -m gpu -x -q --timeout 240 --timeout-method thread -k "bulk_vs_oracle or c2_past or golden" > $OUT/pytest_$v.log 2>&1
+      -m gpu -x -q --timeout 240 --timeout-method thread -k "c2_past or RS_255_223 or (bulk and 223 and not CCSDS)" > $OUT/pytest_$v.log 2>&1
   rc=$?; echo "variant $v parity rc=$rc: $(tail -n 1 $OUT/pytest_$v.log)"; [ $rc -eq 0 ] || exit $rc
 done
 for v in default $VARS; do
