@@ -1117,20 +1117,38 @@ __global__ void __launch_bounds__(512) k_ps_parity8(const uint8_t *ws, size_t ws
     constexpr int NCH = (NR + 7) / 8;
     pt::u32x4 v[NCH][2];
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-        const int i = wave + 8 * c < NR ? wave + 8 * c : 0;   // past NR: a dummy load keeps the
-        {                                                      // per-chunk vmcnt counts uniform
-            asm volatile("global_load_dwordx4 %0, %2, off\n\t"
-                         "global_load_dwordx4 %1, %2, off offset:16"
-                         : "=&v"(v[c][0]), "=&v"(v[c][1]) : "v"(src + i * ws_pitch) : "memory");
-        }
+    for (int c = 0; c < NCH; ++c) {                            // plain loads: the compiler counts
+        const int i = wave + 8 * c < NR ? wave + 8 * c : 0;   // them (past NR: a dummy row 0)
+        v[c][0] = *reinterpret_cast<const pt::u32x4 *>(src + i * ws_pitch);
+        v[c][1] = *reinterpret_cast<const pt::u32x4 *>(src + i * ws_pitch + 16);
+        __builtin_amdgcn_sched_barrier(0);                     // issue order = chunk order
     }
+#ifdef EZRS_PAR_NOCHUNK
+    auto ready = [&](auto cc) {                                // A/B: every chunk before the passes
+        if constexpr (decltype(cc)::value == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            static_for<0, NCH>([&](auto c2) {
+                constexpr int c = decltype(c2)::value;
+                pt::u32x4 a0 = v[c][0], a1 = v[c][1];
+                asm volatile("" : "+v"(a0), "+v"(a1));
+                const int i = wave + 8 * c;
+                if (i < NR) {
+                    uint32_t D[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+                    transpose8(D);
+#pragma unroll
+                    for (int qq = 0; qq < 8; ++qq) lds[(8 * i + qq) * 64 + lane] = D[qq];
+                }
+            });
+            pt::wait_lgkm();
+            pt::barrier();
+        }
+    };
+#else
     auto ready = [&](auto cc) {
         constexpr int c = decltype(cc)::value;
         const int i = wave + 8 * c;
-        pt::u32x4 a0 = v[c][0], a1 = v[c][1];                  // this chunk's two loads landed (the
-        asm volatile("s_waitcnt vmcnt(%2)" : "+v"(a0), "+v"(a1) : "n"(2 * (NCH - 1 - c)) : "memory");
-        if (i < NR) {                                          // registers stay live until then)
+        const pt::u32x4 a0 = v[c][0], a1 = v[c][1];
+        if (i < NR) {
             uint32_t D[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
             transpose8(D);                                     // D[q] bit 8k + m: cw 4m + k
 #pragma unroll
@@ -1139,6 +1157,7 @@ __global__ void __launch_bounds__(512) k_ps_parity8(const uint8_t *ws, size_t ws
         pt::wait_lgkm();                                       // raw barrier: later chunks' loads stay in flight
         pt::barrier();
     };
+#endif
     ready(std::integral_constant<int, 0>{});
     PAR_STAMP(1);
     PAR_STAMP(2);
