@@ -593,9 +593,11 @@ __device__ __forceinline__ void pt_run_lin(const PsArgs &a, uint8_t *lds) {
             barrier();
         }
 #if EZRS_PT_PRIO
-        // main loop priority experiments (timing builds only): 1 = waves 4..7 first, 2 = by quarter
+        // main loop priority experiments (timing builds only): 1 = waves 4..7 first, 2 = by quarter,
+        // 3 = all
         if (EZRS_PT_PRIO == 1 && w >= 4) asm volatile("s_setprio 1");
         if (EZRS_PT_PRIO == 2) { if (w >= 6) asm volatile("s_setprio 3"); else if (w >= 4) asm volatile("s_setprio 2"); else if (w >= 2) asm volatile("s_setprio 1"); }
+        if (EZRS_PT_PRIO == 3) asm volatile("s_setprio 1");  // every main loop over the tails
 #endif
         int tlo = lo;                                        // shard batches: pad of the tile's rows
         if constexpr (SH) {
@@ -910,6 +912,9 @@ __device__ __forceinline__ void wave_tail(uint32_t (&V)[C::NI][8], const PsArgs 
 #pragma unroll
         for (int t = 0; t < 8; ++t) T[i][t] = C::OWN[W][i] >= 0 ? V[C::OWN[W][i] < 0 ? 0 : C::OWN[W][i]][t] : 0u;
     uint32_t Qs[C::NQ][8], nz = 0;
+#ifdef EZRS_PQ_FOLDPRIO
+    asm volatile("s_setprio 1");
+#endif
     C::template epilogue<W>(T, [&](auto qc, uint32_t (&Qw)[8]) {
         constexpr int qd = decltype(qc)::value;
         constexpr uint32_t vm = (C::SYN[W][qd][0] >= 0 ? 0x01010101u : 0u) | (C::SYN[W][qd][1] >= 0 ? 0x02020202u : 0u) |
@@ -929,6 +934,9 @@ __device__ __forceinline__ void wave_tail(uint32_t (&V)[C::NI][8], const PsArgs 
 #endif
     });
     PQ_STAMP(5);
+#ifdef EZRS_PQ_FOLDPRIO
+    asm volatile("s_setprio 0");
+#endif
 #ifdef EZRS_PQ_DMA_LATE
     if (noff != kOob) issue_tile(lbuf, rsrc, noff, nbytes, W);
 #endif
@@ -1051,11 +1059,13 @@ __device__ __forceinline__ void pq_run(const PsArgs &a, uint8_t *lds) {
             if (kt < t0 + kTile && kt < a.ncw) tlo = a.stail_lo;
         }
         PQ_STAMP(1);
-#ifdef EZRS_PQ_PRIO
+#ifndef EZRS_PQ_NOPRIO
+        // the main loop outranks the other workgroup's waves on the SIMD (their exchange, DMA and
+        // fold): r04j C2 1203 vs 1169 GB/s
         asm volatile("s_setprio 1");
 #endif
         pq_pass<C, ENC, W, SH, LO0>(V, lbuf, a.stride, lo, tlo);
-#ifdef EZRS_PQ_PRIO
+#ifndef EZRS_PQ_NOPRIO
         asm volatile("s_setprio 0");
 #endif
         PQ_STAMP(2);
