@@ -50,7 +50,7 @@ constexpr int kN = 255;
 typedef __attribute__((address_space(3))) void lds_void;
 
 #ifndef EZRS_PT_PRIO
-#define EZRS_PT_PRIO 0
+#define EZRS_PT_PRIO 3                // every main loop at s_setprio 1: r04k C2 on k_pt_lin 1115 vs 1091 GB/s
 #endif
 #ifdef EZRS_PS_STAMPS
 // tools/micro/pt_stamps.hip: phase stamps of the linear tile kernel, [wg][wave][tile][phase]
@@ -593,8 +593,8 @@ __device__ __forceinline__ void pt_run_lin(const PsArgs &a, uint8_t *lds) {
             barrier();
         }
 #if EZRS_PT_PRIO
-        // main loop priority experiments (timing builds only): 1 = waves 4..7 first, 2 = by quarter,
-        // 3 = all
+        // main loop priority: 3 (default) = every wave over the other workgroup's tails; timing
+        // builds: 0 = none, 1 = waves 4..7 first, 2 = by quarter
         if (EZRS_PT_PRIO == 1 && w >= 4) asm volatile("s_setprio 1");
         if (EZRS_PT_PRIO == 2) { if (w >= 6) asm volatile("s_setprio 3"); else if (w >= 4) asm volatile("s_setprio 2"); else if (w >= 2) asm volatile("s_setprio 1"); }
         if (EZRS_PT_PRIO == 3) asm volatile("s_setprio 1");  // every main loop over the tails

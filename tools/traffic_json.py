@@ -26,8 +26,9 @@ CALLS = {
 
 
 def kernel_call(name):
-    if "k_pt_lin<" in name:                      # k_pt_lin<codec, ENC, SH>
-        return "ezrs_encode" if name.split("k_pt_lin<")[1].split(",")[1].strip() == "true" else "ezrs_decode"
+    for kn in ("k_pt_lin<", "k_pq_lin<"):        # k_pt_lin / k_pq_lin<codec, ENC, SH, LO0>
+        if kn in name:
+            return "ezrs_encode" if name.split(kn)[1].split(",")[1].strip() == "true" else "ezrs_decode"
     if "k_py_syndromes" in name or "k_pg_syndromes" in name:
         return "ezrs_encode" if "true>" in name else "ezrs_decode"
     for call, keys in (("ezrs_encode", ("k_ps_parity", "k_wide_finish<true>")),
