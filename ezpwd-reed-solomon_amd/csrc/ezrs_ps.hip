@@ -683,6 +683,24 @@ __device__ __forceinline__ void issue_at(Raw &r, const uint32_t (&at4)[4]) {
                      : "v"(at4[k]), "n"(OFF / 4), "n"(OFF / 4 + 1), "n"(OFF / 4 + 2), "n"(OFF / 4 + 3), "n"(OFF + 16)
                      : "memory");
 }
+// a final single-block piece: bytes OFF .. OFF+11 only (the dwords block B+1 would need are not
+// read, so no dead in-flight register is left for the allocator to move)
+template <int OFF>
+__device__ __forceinline__ void issue_half(Raw &r, const uint32_t (&at4)[4]) {
+    static_assert(OFF % 4 == 0 && OFF / 4 + 2 < 256, "ds_read2 dword offsets");
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        asm volatile("ds_read2_b32 %0, %2 offset0:%3 offset1:%4\n\t"
+                     "ds_read_b32 %1, %2 offset:%5"
+                     : "=&v"(r.e[k][0]), "=&v"(r.e[k][1].x) : "v"(at4[k]), "n"(OFF / 4), "n"(OFF / 4 + 1), "n"(OFF + 8)
+                     : "memory");
+    }                                                        // e[k][1].y and d4[k] stay unset
+}
+template <int OFF, bool HALF>
+__device__ __forceinline__ void issue_piece(Raw &r, const uint32_t (&at4)[4]) {
+    if constexpr (HALF) issue_half<OFF>(r, at4);
+    else issue_at<OFF>(r, at4);
+}
 __device__ __forceinline__ void wait_raw(Raw &r) {
     asm volatile("s_waitcnt lgkmcnt(0)"
                  : "+v"(r.e[0][0]), "+v"(r.e[0][1]), "+v"(r.d4[0]), "+v"(r.e[1][0]), "+v"(r.e[1][1]), "+v"(r.d4[1]),
@@ -703,7 +721,7 @@ __device__ __forceinline__ void row_addrs(uint32_t (&at)[4], uint32_t lbuf, uint
 // aligned 16 bytes of each row; shard batches: bytes before a shortened row's own pad masked off
 template <bool SH>
 __device__ __forceinline__ void align_rows(u32x4 (&R)[4], const Raw &r, const uint32_t (&at)[4], int pa,
-                                          int tail_lo, const u32x4 &e) {
+                                          int tail_lo, uint32_t pads) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const uint32_t d[5] = {r.e[k][0].x, r.e[k][0].y, r.e[k][1].x, r.e[k][1].y, r.d4[k]};
@@ -714,7 +732,7 @@ __device__ __forceinline__ void align_rows(u32x4 (&R)[4], const Raw &r, const ui
         if (pa < tail_lo) {                                  // wave-uniform
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const int z8 = 8 * ((int)(e[k] >> 24) - pa);
+                const int z8 = 8 * ((int)((pads >> (8 * k)) & 0xFFu) - pa);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int c = min(max(z8 - 32 * j, 0), 32);
@@ -749,20 +767,21 @@ __device__ __forceinline__ void block8(uint32_t (&V)[C::NI][8], uint32_t (&X)[8]
 // issue the next piece's, run its networks.
 template <class C, bool ENC, int W, bool SH, bool LO0, int I>
 __device__ __forceinline__ void piece(uint32_t (&V)[C::NI][8], Raw &cur, const uint32_t (&at)[4],
-                                      const uint32_t (&at4)[4], int lo, int tail_lo, const u32x4 &e) {
+                                      const uint32_t (&at4)[4], int lo, int tail_lo, uint32_t pads) {
     constexpr int E = ENC ? 1 : 0;
     constexpr int HI = ENC ? kN - (int)C::NR : kN;
-    constexpr int b0 = C::B0[E][W], b1 = C::B0[E][W + 1];
+    // blocks at or past HI (encode: the parity positions) are neither read nor run
+    constexpr int b0 = C::B0[E][W], b1 = C::B0[E][W + 1] < (HI + 7) / 8 ? C::B0[E][W + 1] : (HI + 7) / 8;
     constexpr int B = b0 + 2 * I;
     if constexpr (B < b1) {
         wait_raw(cur);
         Raw nxt;
 #ifndef EZRS_PQ_NOPREFETCH
-        if constexpr (B + 2 < b1) issue_at<8 * (B + 2)>(nxt, at4);
+        if constexpr (B + 2 < b1) issue_piece<8 * (B + 2), (B + 3 >= b1)>(nxt, at4);
 #endif
         __builtin_amdgcn_sched_barrier(0);
         u32x4 R[4];
-        align_rows<SH>(R, cur, at, 8 * B, tail_lo, e);
+        align_rows<SH>(R, cur, at, 8 * B, tail_lo, pads);
         uint32_t X[8];
         {
             const uint32_t c0[4] = {R[0].x, R[1].x, R[2].x, R[3].x};
@@ -781,9 +800,9 @@ __device__ __forceinline__ void piece(uint32_t (&V)[C::NI][8], Raw &cur, const u
         }
         __builtin_amdgcn_sched_barrier(0);
 #ifdef EZRS_PQ_NOPREFETCH
-        if constexpr (B + 2 < b1) issue_at<8 * (B + 2)>(nxt, at4);
+        if constexpr (B + 2 < b1) issue_piece<8 * (B + 2), (B + 3 >= b1)>(nxt, at4);
 #endif
-        if constexpr (B + 2 < b1) piece<C, ENC, W, SH, LO0, I + 1>(V, nxt, at, at4, lo, tail_lo, e);
+        if constexpr (B + 2 < b1) piece<C, ENC, W, SH, LO0, I + 1>(V, nxt, at, at4, lo, tail_lo, pads);
     }
 }
 
@@ -800,8 +819,12 @@ __device__ __forceinline__ void pq_pass(uint32_t (&V)[C::NI][8], uint32_t lbuf, 
     row_addrs<SH>(at, lbuf, stride, lo, e);
 #pragma unroll
     for (int k = 0; k < 4; ++k) at4[k] = at[k] & ~3u;        // byte phase at[k] & 3 for v_alignbyte
-    issue_at<8 * b0>(cur, at4);
-    piece<C, ENC, W, SH, LO0, 0>(V, cur, at, at4, lo, tail_lo, e);
+    // shard batches: the four rows' pads, one byte each (the row table entry is dead after this)
+    const uint32_t pads = SH ? (e[0] >> 24) | (e[1] >> 24) << 8 | (e[2] >> 24) << 16 | (e[3] >> 24) << 24 : 0u;
+    constexpr int HI = ENC ? kN - (int)C::NR : kN;
+    constexpr int b1 = C::B0[E][W + 1] < (HI + 7) / 8 ? C::B0[E][W + 1] : (HI + 7) / 8;
+    issue_piece<8 * b0, (b0 + 1 >= b1)>(cur, at4);
+    piece<C, ENC, W, SH, LO0, 0>(V, cur, at, at4, lo, tail_lo, pads);
 }
 
 // Recursive-halving exchange (partner W ^ (1 << XR[s])), slots of XCAP items x 2 KiB per wave.
