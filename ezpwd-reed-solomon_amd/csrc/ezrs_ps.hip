@@ -65,8 +65,14 @@ __device__ unsigned long long g_pq_stamps[16][4][8][8];
     __builtin_amdgcn_sched_barrier(0); } while (0)
 // tools/micro/par_stamps.hip: the parity kernel's phases, [block][wave][phase]
 __device__ unsigned long long g_par_stamps[64][8][8];
-#define PAR_STAMP(ph) do { __builtin_amdgcn_sched_barrier(0); if (blockIdx.x < 64 && __lane_id() == 0) \
-    g_par_stamps[blockIdx.x][wave][ph] = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
+__device__ unsigned long long g_par_rt[4096][2];           // s_memrealtime (100 MHz) at wave 0's start / end
+__device__ unsigned g_par_hw[4096];                        // HW_ID of wave 0
+#define PAR_STAMP(ph) do { __builtin_amdgcn_sched_barrier(0); if (__lane_id() == 0) { \
+    if (blockIdx.x < 64) g_par_stamps[blockIdx.x][wave][ph] = __builtin_amdgcn_s_memtime(); \
+    if (wave == 0 && (ph == 0 || ph == 7) && blockIdx.x < 4096) { \
+        g_par_rt[blockIdx.x][ph == 7] = __builtin_amdgcn_s_memrealtime(); \
+        if (ph == 0) g_par_hw[blockIdx.x] = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11)); } } \
+    __builtin_amdgcn_sched_barrier(0); } while (0)
 #else
 #define PT_STAMP(ph) do { } while (0)
 #define PQ_STAMP(ph) do { } while (0)

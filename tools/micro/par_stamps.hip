@@ -38,6 +38,28 @@ int main() {
         for (int ph = 0; ph < 7; ++ph) { printf(" %s %6.0f", names[ph], acc[w][ph] / 64); tot += acc[w][ph] / 64; }
         printf("  | total %6.0f\n", tot);
     }
+    static unsigned long long rt[4096][2];
+    static unsigned hw[4096];
+    (void)hipMemcpyFromSymbol(rt, HIP_SYMBOL(ps::g_par_rt), sizeof rt);
+    (void)hipMemcpyFromSymbol(hw, HIP_SYMBOL(ps::g_par_hw), sizeof hw);
+    unsigned long long r0 = ~0ull, r1 = 0;
+    for (unsigned b = 0; b < grid; ++b) { r0 = rt[b][0] < r0 ? rt[b][0] : r0; r1 = rt[b][1] > r1 ? rt[b][1] : r1; }
+    printf("realtime (100 MHz ticks = 10 ns): first start .. last end %llu ticks\n", r1 - r0);
+    int hist_s[64] = {}, hist_d[64] = {};
+    double dsum = 0;
+    for (unsigned b = 0; b < grid; ++b) {
+        const unsigned long long s_ = (rt[b][0] - r0) / 100, d = (rt[b][1] - rt[b][0]) / 100;  // us
+        hist_s[s_ < 63 ? s_ : 63]++;
+        hist_d[d < 63 ? d : 63]++;
+        dsum += (double)(rt[b][1] - rt[b][0]) / 100.0;
+    }
+    printf("block durations: mean %.2f us\nstart-time histogram (us: count):", dsum / grid);
+    for (int i = 0; i < 64; ++i) if (hist_s[i]) printf(" %d:%d", i, hist_s[i]);
+    printf("\nduration histogram (us: count):");
+    for (int i = 0; i < 64; ++i) if (hist_d[i]) printf(" %d:%d", i, hist_d[i]);
+    printf("\nHW_ID of blocks 0..15:");
+    for (int b = 0; b < 16; ++b) printf(" %08x", hw[b]);
+    printf("\n");
     unsigned long long s0[64];
     for (int blk = 0; blk < 64; ++blk) s0[blk] = st[blk][0][0] - t0;
     printf("block start offsets:");
