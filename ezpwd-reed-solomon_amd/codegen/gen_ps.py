@@ -145,9 +145,9 @@ def mat_apply(out, dst, src, rows, ind, extra=None):
 
 def gen_parity(c: PsCodec):
     """PS_<codec>: the codec's constants and the parity map passes over 32-codeword bit-sliced
-    syndromes, q_pass4<P> = parity symbols 4P .. 4P+3 (k_ps_parity8, wave P).  The planes of
-    syndromes 8c .. 8c+7 arrive as chunk c: before its first read of chunk c >= 1 a pass calls
-    ready(std::integral_constant<int, c>) (k_ps_parity8 stages its loads by chunk)."""
+    syndromes, q_pass4<P> = parity symbols 4P .. 4P+3 (k_ps_parity8, wave P).  Before it reads
+    syndrome i's planes (i >= 1) a pass calls ready(std::integral_constant<int, i>): the kernel
+    makes staged planes visible there, and interleaves other work (k_ps_parity8)."""
     st = f"PS_{c.name}"
     npass = (c.nr + 3) // 4
     out = [f"struct {st} {{",
@@ -178,8 +178,7 @@ def gen_parity(c: PsCodec):
             out.append(f"{I}    #pragma unroll")
             out.append(f"{I}    for (int q = 0; q < 8; ++q) P[q] = N[q];")
             if i + 1 < nr:
-                if (i + 1) % 8 == 0:
-                    out.append(f"{I}    ready(std::integral_constant<int, {(i + 1) // 8}>{{}});")
+                out.append(f"{I}    ready(std::integral_constant<int, {i + 1}>{{}});")
                 out.append(f"{I}    #pragma unroll")
                 out.append(f"{I}    for (int q = 0; q < 8; ++q) N[q] = in[({8 * (i + 1)} + q) * ld];")
             out.append(f"{I}    __builtin_amdgcn_sched_barrier(0);")

@@ -1136,6 +1136,146 @@ k_pq_lin(PsArgs a) {
 constexpr int kParGroups = 64;
 constexpr int kParCw = 32 * kParGroups;
 
+// wave P runs pass P (parity symbols 4P .. 4P+3) with hook H
+template <class C, class H>
+__device__ __forceinline__ void pass_switch(int wave, uint32_t (&O)[4][8], const uint32_t *in, H &hook) {
+    switch (wave) {
+    case 0: C::template q_pass4<0>(O, in, 64, hook); break;
+    case 1: if constexpr (C::NPASS4 > 1) C::template q_pass4<1>(O, in, 64, hook); break;
+    case 2: if constexpr (C::NPASS4 > 2) C::template q_pass4<2>(O, in, 64, hook); break;
+    case 3: if constexpr (C::NPASS4 > 3) C::template q_pass4<3>(O, in, 64, hook); break;
+    case 4: if constexpr (C::NPASS4 > 4) C::template q_pass4<4>(O, in, 64, hook); break;
+    case 5: if constexpr (C::NPASS4 > 5) C::template q_pass4<5>(O, in, 64, hook); break;
+    case 6: if constexpr (C::NPASS4 > 6) C::template q_pass4<6>(O, in, 64, hook); break;
+    default: if constexpr (C::NPASS4 > 7) C::template q_pass4<7>(O, in, 64, hook); break;
+    }
+}
+
+// Codeword k's parity row: 8/4/1-byte copies of the staged row s8.
+template <int NR>
+__device__ __forceinline__ void store_parity_row(uint8_t *dst, const uint8_t *s8) {
+    if constexpr (NR % 8 == 0) {
+#pragma unroll
+        for (int o = 0; o < NR; o += 8) {
+            uint2 v = *reinterpret_cast<const uint2 *>(s8 + o);
+            __builtin_memcpy(dst + o, &v, 8);
+        }
+    } else if constexpr (NR % 4 == 0) {
+#pragma unroll
+        for (int o = 0; o < NR; o += 4) {
+            uint32_t v = *reinterpret_cast<const uint32_t *>(s8 + o);
+            __builtin_memcpy(dst + o, &v, 4);
+        }
+    } else {
+        for (int o = 0; o < NR; ++o) dst[o] = s8[o];
+    }
+}
+
+// Persistent, software-pipelined form of k_ps_parity8 (one 8-wave block per CU: planes and stage
+// in separate LDS, 130 KiB): chunk j's map runs while chunk j-1's parity rows drain to memory
+// (one quarter of the stores at each of four points of the pass) and chunk j+1's syndromes load
+// (issued once chunk j's last planes are written).  In k_ps_parity8 every block maps, then
+// stores, in lockstep with all the others (r04l stamps: map 10.8 us, stores 4-10 us, serial).
+template <class C>
+__global__ void __launch_bounds__(512) k_ps_parity_pipe(const uint8_t *ws, size_t ws_pitch, uint8_t *parity,
+                                                        size_t pstride, size_t ncw, Shards sh, unsigned len,
+                                                        unsigned nchunk) {
+    constexpr int NR = C::NR;
+    constexpr int kRegion = 32 * NR + 8;
+    constexpr int kPlanes = 8 * NR * kParGroups;               // dwords
+    constexpr int kStage = kParGroups * kRegion / 4;           // dwords
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kPlanes + kStage];
+    uint8_t *stage = reinterpret_cast<uint8_t *>(lds + kPlanes);
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    constexpr int NCH = (NR + 7) / 8;
+    constexpr int IL = 8 * (NCH - 1);                          // hooks 1 .. IL spread chunk j-1's stores
+    pt::u32x4 v[NCH][2];
+    auto load = [&](unsigned chunk) {
+        const uint8_t *src = ws + ((size_t)chunk * kParGroups + lane) * 32;
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            const int i = wave + 8 * c < NR ? wave + 8 * c : 0;
+            v[c][0] = *reinterpret_cast<const pt::u32x4 *>(src + i * ws_pitch);
+            v[c][1] = *reinterpret_cast<const pt::u32x4 *>(src + i * ws_pitch + 16);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    // every chunk's planes at once: a store in flight makes the compiler drain vmcnt to 0 at the
+    // next wait on a load (stores may complete out of order), so the planes are all in LDS before
+    // the pass interleaves the stores
+    auto ready_all = [&]() {
+        static_for<0, NCH>([&](auto cc) {
+            constexpr int c = decltype(cc)::value;
+            const int i = wave + 8 * c;
+            const pt::u32x4 a0 = v[c][0], a1 = v[c][1];
+            if (i < NR) {
+                uint32_t D[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+                transpose8(D);
+#pragma unroll
+                for (int qq = 0; qq < 8; ++qq) lds[(8 * i + qq) * 64 + lane] = D[qq];
+            }
+        });
+        pt::wait_lgkm();
+        pt::barrier();
+    };
+    auto store_part = [&](unsigned chunk, int j) {             // rows 512 j .. 512 j + 511 of a chunk
+        const int r = threadIdx.x + 512 * j;
+        const size_t k = (size_t)chunk * kParCw + r;
+        if (k < ncw) {
+            unsigned rlen;
+            uint8_t *dst = sh.rows ? parity + shard_row(sh, k, pstride, len, rlen) + rlen : parity + k * pstride;
+            store_parity_row<NR>(dst, stage + (r >> 5) * kRegion + (r & 31) * NR);
+        }
+    };
+    unsigned chunk = blockIdx.x, prev = 0xFFFFFFFFu;
+    if (chunk < nchunk) load(chunk);
+    for (; chunk < nchunk; chunk += gridDim.x) {
+        const unsigned next = chunk + gridDim.x;
+        ready_all();
+        auto hook = [&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            // chunk j-1's rows, a quarter at each of four points of the pass
+            static_for<0, 4>([&](auto jc) {
+                constexpr int jj = decltype(jc)::value;
+                if constexpr (IL > 0 && i == (jj + 1) * IL / 5)
+                    if (prev != 0xFFFFFFFFu) store_part(prev, jj);
+            });
+        };
+        uint32_t O[4][8];
+        pass_switch<C>(wave, O, lds + lane, hook);
+        if (wave >= C::NPASS4) static_for<1, NR>([&](auto ic) { hook(ic); });
+        if constexpr (IL == 0)                                 // no hook points: after the pass
+            if (prev != 0xFFFFFFFFu)
+                for (int j = 0; j < 4; ++j) store_part(prev, j);
+        pt::wait_lgkm();                                       // planes consumed, chunk j-1's stage read
+        pt::barrier();                                         // (raw barriers: loads stay in flight)
+        if (next < nchunk) load(next);                         // in flight through the stage phase
+        if (wave < C::NPASS4) {
+            const int nj = NR - 4 * wave < 4 ? NR - 4 * wave : 4;
+#pragma unroll
+            for (int jl = 0; jl < 4; ++jl)
+                if (jl < nj) transpose8(O[jl]);
+            uint8_t *reg = stage + lane * kRegion + 4 * wave;
+#pragma unroll
+            for (int m = 0; m < 8; ++m)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    uint8_t *row = reg + (4 * m + k) * NR;
+                    if (nj == 4) {
+                        *reinterpret_cast<uint32_t *>(row) = gather4(O[0][m], O[1][m], O[2][m], O[3][m], k);
+                    } else {
+                        for (int jl = 0; jl < nj; ++jl) row[jl] = (uint8_t)(O[jl][m] >> (8 * k));
+                    }
+                }
+        }
+        pt::wait_lgkm();                                       // stage complete
+        pt::barrier();
+        prev = chunk;
+    }
+    if (prev != 0xFFFFFFFFu)
+        for (int j = 0; j < 4; ++j) store_part(prev, j);
+}
+
 // 8-wave form of k_ps_parity: wave P computes parity symbols 4P..4P+3 (q_pass4), halving each
 // wave's share of the map and doubling the waves that hide the phases' latencies.
 template <class C>
@@ -1200,19 +1340,14 @@ __global__ void __launch_bounds__(512) k_ps_parity8(const uint8_t *ws, size_t ws
     ready(std::integral_constant<int, 0>{});
     PAR_STAMP(1);
     PAR_STAMP(2);
+    auto hook = [&](auto ic) {                                 // before syndrome i: chunk i / 8
+        constexpr int i = decltype(ic)::value;
+        if constexpr (i % 8 == 0) ready(std::integral_constant<int, i / 8>{});
+    };
     uint32_t O[4][8];
-    switch (wave) {
-    case 0: C::template q_pass4<0>(O, lds + lane, 64, ready); break;
-    case 1: if constexpr (C::NPASS4 > 1) C::template q_pass4<1>(O, lds + lane, 64, ready); break;
-    case 2: if constexpr (C::NPASS4 > 2) C::template q_pass4<2>(O, lds + lane, 64, ready); break;
-    case 3: if constexpr (C::NPASS4 > 3) C::template q_pass4<3>(O, lds + lane, 64, ready); break;
-    case 4: if constexpr (C::NPASS4 > 4) C::template q_pass4<4>(O, lds + lane, 64, ready); break;
-    case 5: if constexpr (C::NPASS4 > 5) C::template q_pass4<5>(O, lds + lane, 64, ready); break;
-    case 6: if constexpr (C::NPASS4 > 6) C::template q_pass4<6>(O, lds + lane, 64, ready); break;
-    default: if constexpr (C::NPASS4 > 7) C::template q_pass4<7>(O, lds + lane, 64, ready); break;
-    }
+    pass_switch<C>(wave, O, lds + lane, hook);
     if (wave >= C::NPASS4)                                     // no pass: still takes every barrier
-        static_for<1, NCH>([&](auto cc) { ready(cc); });
+        static_for<1, NR>([&](auto ic) { hook(ic); });
     PAR_STAMP(3);
     __syncthreads();                                           // planes consumed
     PAR_STAMP(4);
@@ -1246,22 +1381,7 @@ __global__ void __launch_bounds__(512) k_ps_parity8(const uint8_t *ws, size_t ws
         unsigned rlen;
         // shard batches: parity is the base of the rows, each row's parity after its data
         uint8_t *dst = sh.rows ? parity + shard_row(sh, k, pstride, len, rlen) + rlen : parity + k * pstride;
-        const uint8_t *s8 = stage + (r >> 5) * kRegion + (r & 31) * NR;
-        if constexpr (NR % 8 == 0) {
-#pragma unroll
-            for (int o = 0; o < NR; o += 8) {
-                uint2 v = *reinterpret_cast<const uint2 *>(s8 + o);
-                __builtin_memcpy(dst + o, &v, 8);
-            }
-        } else if constexpr (NR % 4 == 0) {
-#pragma unroll
-            for (int o = 0; o < NR; o += 4) {
-                uint32_t v = *reinterpret_cast<const uint32_t *>(s8 + o);
-                __builtin_memcpy(dst + o, &v, 4);
-            }
-        } else {
-            for (int o = 0; o < NR; ++o) dst[o] = s8[o];
-        }
+        store_parity_row<NR>(dst, stage + (r >> 5) * kRegion + (r & 31) * NR);
     }
     PAR_STAMP(7);
 }
@@ -1274,6 +1394,23 @@ namespace {
 template <class C> bool ps_matches(const DevCodec &d) {
     return d.mm == 8 && d.nroots == C::NR && d.fcr == C::FCR && d.prim == C::PRIM && !d.dual &&
            d.poly == C::POLY;
+}
+
+// The parity stage: k_ps_parity8, one block per chunk (default), or the pipelined persistent
+// kernel, one block per CU over the chunks (-DEZRS_PAR_PIPE, A/B builds: r04n 44.2 vs 41.2 us --
+// at two waves per SIMD the map loses more than the overlapped stores save).
+template <class PS>
+void launch_parity(const DevCodec &d, const uint8_t *ws, size_t ws_pitch, uint8_t *par, size_t pstride,
+                   size_t n, const Shards &sh, unsigned len, unsigned nchunk, hipStream_t s) {
+#ifndef EZRS_PAR_PIPE
+    (void)d;
+    hipLaunchKernelGGL((ps::k_ps_parity8<PS>), dim3(nchunk), dim3(512), 0, s, ws, ws_pitch, par, pstride, n, sh, len);
+#else
+    const unsigned ncu = d.ncu > 0 ? (unsigned)d.ncu : 256u;
+    const unsigned g = nchunk < ncu ? nchunk : ncu;
+    hipLaunchKernelGGL((ps::k_ps_parity_pipe<PS>), dim3(g), dim3(512), 0, s, ws, ws_pitch, par, pstride, n, sh, len,
+                       nchunk);
+#endif
 }
 
 // Workgroups per launch (persistent over tiles): 2 per CU (80 KiB LDS each).
@@ -1425,9 +1562,8 @@ hipError_t launch_ps_encode(int id, const DevCodec &d, const EncodeArgs &a, void
         if (k++ == id) {                                                                          \
             const unsigned pgrid = (unsigned)((n + ps::kParCw - 1) / ps::kParCw);                 \
             launch_tile<ps::PS_##C, ps::PT_##C, true>(p, a.sh.rows != 0, grid, s);                \
-            hipLaunchKernelGGL((ps::k_ps_parity8<ps::PS_##C>), dim3(pgrid), dim3(512), 0, s,      \
-                               static_cast<const uint8_t *>(ws), p.ws_pitch, par, a.parity_stride, n, \
-                               a.sh, a.len);                                                      \
+            launch_parity<ps::PS_##C>(d, static_cast<const uint8_t *>(ws), p.ws_pitch, par,     \
+                                      a.parity_stride, n, a.sh, a.len, pgrid, s);                 \
         }
         EZRS_PS_CODEC_LIST(EZRS_PS_ENC)
 #undef EZRS_PS_ENC
