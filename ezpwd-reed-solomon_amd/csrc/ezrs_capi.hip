@@ -9,7 +9,6 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
-#include <atomic>
 #include <new>
 #include <string>
 #include <thread>
@@ -46,7 +45,6 @@ struct ezrs_codec {
         void *p = nullptr;
         size_t bytes = 0;
     };
-    mutable std::atomic<uint32_t> dec_seq{0};         // decode calls on the sliced path (DecodeArgs::seq)
     mutable std::mutex ws_mu;
     mutable std::unordered_map<void *, Ws> ws;
     mutable std::vector<void *> ws_retired;
@@ -307,13 +305,8 @@ hipError_t dispatch_decode(const ezrs_codec *c, const DecodeArgs &a, uint8_t *sy
     const bool contiguous = a.parity == static_cast<char *>(a.data) + (size_t)a.len * w &&
                             a.parity_stride == a.data_stride;
     if (c->ps_id >= 0 && ps_can_decode(c->dev, a)) {
-        DecodeArgs b = a;
-        b.any = reinterpret_cast<const uint32_t *>(syn_ws + ps_any_offset(a.ncw));
-        uint32_t q;
-        while ((q = c->dec_seq.fetch_add(1, std::memory_order_relaxed) + 1) == 0) {}
-        b.seq = q;                                          // unique per call (0 never used)
-        hipError_t e = launch_ps_syndromes(c->ps_id, c->dev, b, syn_ws, st);
-        if (e == hipSuccess) e = launch_decode_flagged(c->dev, b, syn_ws, SynLayout::Tiled, st);
+        hipError_t e = launch_ps_syndromes(c->ps_id, c->dev, a, syn_ws, st);
+        if (e == hipSuccess) e = launch_decode_flagged(c->dev, a, syn_ws, SynLayout::Tiled, st);
         return e;
     }
     if (a.sh.rows) return launch_decode_generic(c->dev, a, st);     // shard rows: per-codeword kernels

@@ -388,7 +388,6 @@ __device__ __forceinline__ unsigned screen(const DecodeArgs &a, size_t sp, unsig
 __global__ void __launch_bounds__(64 * kWaves) k_decode_errors(DevCodec c, DecodeArgs a, const uint8_t *syn_ws,
                                                               SynLayout layout) {
     __shared__ __attribute__((aligned(16))) Lds L;
-    if (a.any && !a.neras && *a.any != a.seq) return;          // the syndrome pass flagged nothing
     const unsigned lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const size_t nspan = (a.ncw + kSpan - 1) / kSpan, step = (size_t)gridDim.x * kWaves;
     unsigned any = 0;

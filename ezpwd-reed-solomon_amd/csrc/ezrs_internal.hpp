@@ -77,10 +77,6 @@ struct DecodeArgs {
     size_t corr_stride;
     size_t ncw;
     Shards sh{};                  // sh.rows != 0: shard rows, parity inline (data + row length)
-    // plane-sliced path: the syndrome kernel stores seq at *any when it flags a codeword, so the
-    // error path leaves at once when nothing was flagged (and no erasures came with the batch)
-    const uint32_t *any = nullptr;
-    uint32_t seq = 0;
 };
 
 struct EncodeArgs {
@@ -134,7 +130,6 @@ hipError_t launch_bs_syndromes(int id, const DevCodec &d, const DecodeArgs &a, u
 // <= 256 bytes; decode needs the parity inside the row.
 int planeslice_codec_id(const DevCodec &d);   // -1 if the codec has no plane-sliced path
 size_t ps_ws_bytes(size_t ncw);
-size_t ps_any_offset(size_t ncw);
 bool ps_can_encode(const DevCodec &d, const EncodeArgs &a);
 bool ps_can_decode(const DevCodec &d, const DecodeArgs &a);
 hipError_t launch_ps_encode(int id, const DevCodec &d, const EncodeArgs &a, void *ws, hipStream_t s);

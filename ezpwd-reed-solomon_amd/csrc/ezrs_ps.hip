@@ -95,8 +95,6 @@ struct PsArgs {
     uint32_t spitch;            // shard pitch in bytes
     int ablate;                 // timing experiments only (tools/pt_ablate.py, EZRS_PT_ABLATE): bit 0
                                 // no main loop, 1 no exchange, 2 no fold, 3 no DMA, 5 nothing flagged
-    uint32_t *any;              // decode: seq is stored here when a tile flags a codeword (DecodeArgs)
-    uint32_t seq;
 };
 
 template <int I, int N, class F> __device__ __forceinline__ void static_for(F &&f) {
@@ -181,7 +179,6 @@ __device__ __forceinline__ uint32_t fresh(uint32_t = 0) {
     return l;
 }
 
-__device__ __forceinline__ bool pt_lane0() { return fresh() == 0; }
 template <int N> __device__ __forceinline__ void wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");
 }
@@ -508,7 +505,6 @@ __device__ __forceinline__ void wave_tail_lin(uint32_t (&V)[C::NI][8], const PsA
                 store_dword(rout, (cw0 + k) * 4u, (fl >> k & 1) ? (uint32_t)kSentinel : 0u);
         }
         if (__ballot(fl != 0) != 0) {                        // flagged codewords: their syndromes
-            if (a.any && pt::pt_lane0()) a.any[0] = a.seq;
             transpose8(Qs);                                  // Qs[jj] byte k: syndrome jj, codeword k
             // tiled layout (ezrs_internal.hpp kSynTile): syndrome j of the 256 codewords of a tile in
             // one 256-byte row, so a lane's four codewords are one dword (unflagged ones included)
@@ -1008,7 +1004,6 @@ __device__ __forceinline__ void wave_tail(uint32_t (&V)[C::NI][8], const PsArgs 
                 pt::store_dword(rout, (cw0 + k) * 4u, (fl >> k & 1) ? (uint32_t)kSentinel : 0u);
         }
         if (__ballot(fl != 0) != 0) {                        // flagged codewords: their syndromes
-            if (a.any && pt::pt_lane0()) a.any[0] = a.seq;
             static_for<0, C::NQ>([&](auto qc) {
                 constexpr int qd = decltype(qc)::value;
                 transpose8(Qs[qd]);
@@ -1490,9 +1485,7 @@ static int pt_ablate() {
 // Workspace: decode tiled syndromes (kSynTile); encode [NR][ws_pitch] syndromes, ws_pitch = ncw
 // rounded up to 2048 (the parity kernel's block).
 static size_t ps_pitch(size_t ncw) { return (ncw + 2047) / 2048 * 2048; }
-// syndromes (either layout) + the decode's flagged-anything word (ps_any_offset)
-size_t ps_ws_bytes(size_t ncw) { return ps_pitch(ncw) * 32 + 256; }
-size_t ps_any_offset(size_t ncw) { return ps_pitch(ncw) * 32; }
+size_t ps_ws_bytes(size_t ncw) { return ps_pitch(ncw) * 32; }
 
 // Largest batch one launch takes: every buffer offset stays below 0xF0000000 (32-bit offsets;
 // the tile kernel's out-of-range marker kOob is above them).
@@ -1604,8 +1597,6 @@ hipError_t launch_ps_syndromes(int id, const DevCodec &d, const DecodeArgs &a, u
         p.ws = syn_ws + k0 / 256 * kSynTile;                  // tiled layout, global codeword index
         p.ws_pitch = k0 % 256;
         p.ablate = pt_ablate();
-        p.any = const_cast<uint32_t *>(a.any);
-        p.seq = a.seq;
         const unsigned grid = syn_grid(d, p.ntiles);
         int k = 0;
 #define EZRS_PS_SYN(C)                                                                            \
