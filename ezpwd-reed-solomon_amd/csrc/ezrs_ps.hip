@@ -735,15 +735,21 @@ __device__ __forceinline__ void align_rows(u32x4 (&R)[4], const Raw &r, const ui
         for (int j = 0; j < 4; ++j) R[k][j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], at[k]);
     }
     if constexpr (SH) {
+        // bytes before a shortened row's own first byte (the previous row's, in the linear image):
+        // every shard's last row has the same pad tail_lo, so the byte masks are wave-uniform and a
+        // row only selects them (rows with the batch's pad lo are masked by block8 when lo > 0)
         if (pa < tail_lo) {                                  // wave-uniform
+            uint32_t mt[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int c = min(max(8 * (tail_lo - pa) - 32 * j, 0), 32);
+                mt[j] = __builtin_amdgcn_readfirstlane((uint32_t)(0xFFFFFFFFull << c));
+            }
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const int z8 = 8 * ((int)((pads >> (8 * k)) & 0xFFu) - pa);
+                const uint32_t keep = ((pads >> (8 * k)) & 0xFFu) == (uint32_t)tail_lo ? 0u : 0xFFFFFFFFu;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int c = min(max(z8 - 32 * j, 0), 32);
-                    R[k][j] &= (uint32_t)(0xFFFFFFFFull << c);
-                }
+                for (int j = 0; j < 4; ++j) R[k][j] &= keep | mt[j];
             }
         }
     }
