@@ -55,7 +55,15 @@ __host__ __device__ __forceinline__ size_t shard_row(const Shards &g, size_t k, 
         rlen = len;
         return k * stride;
     }
-    const size_t s = k / g.rows, j = k - s * g.rows;
+    size_t s, j;
+    if ((k >> 32) == 0) {                           // 32-bit division (the device's 64-bit one is a
+        const uint32_t k32 = (uint32_t)k, s32 = k32 / g.rows;     // long software sequence)
+        s = s32;
+        j = k32 - s32 * g.rows;
+    } else {
+        s = k / g.rows;
+        j = k - s * g.rows;
+    }
     rlen = j + 1 == g.rows ? g.tail : len;
     return s * g.pitch + j * stride;
 }
