@@ -49,6 +49,9 @@ constexpr int kN = 255;
 
 typedef __attribute__((address_space(3))) void lds_void;
 
+#ifndef EZRS_PQ_MAINPRIO
+#define EZRS_PQ_MAINPRIO 1
+#endif
 #ifndef EZRS_PT_PRIO
 #define EZRS_PT_PRIO 3                // every main loop at s_setprio 1: r04k C2 on k_pt_lin 1115 vs 1091 GB/s
 #endif
@@ -948,7 +951,7 @@ __device__ __forceinline__ void wave_tail(uint32_t (&V)[C::NI][8], const PsArgs 
         for (int t = 0; t < 8; ++t) T[i][t] = C::OWN[W][i] >= 0 ? V[C::OWN[W][i] < 0 ? 0 : C::OWN[W][i]][t] : 0u;
     uint32_t Qs[C::NQ][8], nz = 0;
 #ifdef EZRS_PQ_FOLDPRIO
-    asm volatile("s_setprio 1");
+    asm volatile("s_setprio %0" :: "n"(EZRS_PQ_FOLDPRIO));
 #endif
     C::template epilogue<W>(T, [&](auto qc, uint32_t (&Qw)[8]) {
         constexpr int qd = decltype(qc)::value;
@@ -1097,7 +1100,7 @@ __device__ __forceinline__ void pq_run(const PsArgs &a, uint8_t *lds) {
 #ifndef EZRS_PQ_NOPRIO
         // the main loop outranks the other workgroup's waves on the SIMD (their exchange, DMA and
         // fold): r04j C2 1203 vs 1169 GB/s
-        asm volatile("s_setprio 1");
+        asm volatile("s_setprio %0" :: "n"(EZRS_PQ_MAINPRIO));
 #endif
         pq_pass<C, ENC, W, SH, LO0>(V, lbuf, a.stride, lo, tlo);
 #ifndef EZRS_PQ_NOPRIO
