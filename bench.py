@@ -675,8 +675,10 @@ def bench_shards(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100,
+                    help="timed steps (default 100: the timed region's fixed launch and sync cost "
+                         "is then <1 %% of it)")
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--ncw", type=int, default=1 << 20, help="codewords per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=3.0,
