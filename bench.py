@@ -41,15 +41,34 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+SHARE_GPUS = False              # --share-gpus: ranks may share a GPU (harness test only)
+
+
 def bench_device(local):
-    """This rank's GPU: LOCAL_RANK on a node with a GPU per rank; ranks beyond the visible GPUs wrap
-    around (a one-GPU box running --gpus 2 puts both ranks on cuda:0, which only the harness test
-    does).  The process group is gloo on CPU: the only cross-rank traffic is the barrier and the
-    scalar max/sum of the timing rule, so no RCCL communicator is ever needed."""
+    """This rank's GPU: LOCAL_RANK, one GPU per rank.  More ranks than visible GPUs is an error
+    unless --share-gpus was given (tests/test_bench_gpu.py runs --gpus 2 on a one-GPU box): then
+    ranks wrap around the devices and the JSON line says so (gpu_fields).  The process group is gloo
+    on CPU: the only cross-rank traffic is the barrier and the scalar max/sum of the timing rule, so
+    no RCCL communicator is ever needed."""
     import torch
-    dev = local % max(1, torch.cuda.device_count())
+    ndev = max(1, torch.cuda.device_count())
+    if local >= ndev and not SHARE_GPUS:
+        raise SystemExit(f"bench: LOCAL_RANK {local} but only {ndev} visible GPU(s); one rank per "
+                         "GPU is required (--share-gpus lets ranks share GPUs, never a scaling run)")
+    dev = local % ndev
     torch.cuda.set_device(dev)
     return dev
+
+
+def gpu_fields(world):
+    """n_gpus / scaling of the JSON line: the distinct devices the ranks ran on.  A run whose ranks
+    share GPUs (--share-gpus) is marked so that it is never read as a scaling measurement."""
+    import torch
+    ndev = max(1, torch.cuda.device_count())
+    if world <= ndev:
+        return {"n_gpus": world, "scaling": "weak"}
+    return {"n_gpus": ndev, "ranks": world, "shared_gpus": True,
+            "scaling": "none (ranks share GPUs: harness check, not a scaling measurement)"}
 
 
 def host_cpu_info():
@@ -321,9 +340,9 @@ def bench_rs_errors(args):
         print(json.dumps({
             "metric": f"RS({n},{k}) encode + 8-error/4-erasure decode GB/s device-resident "
                       f"({args.workload.upper()})",
-            "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+            "value": round(value, 3), "unit": "GB/s", **gpu_fields(world), "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(t, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u8" if c3 else "u16",
+            "vs_baseline": None, "dtype": "u8" if c3 else "u16",
             "data": "synthetic",
             "config": {"workload": f"{args.workload.upper()}: RS({n},{k}) encode + decode of 8 errors "
                                    f"+ 4 erasures per codeword (restore copy excluded)",
@@ -407,9 +426,9 @@ def bench_c5(args):
     if rank == 0:
         print(json.dumps({
             "metric": "BCH(1023,983,4) encode+decode GB/s device-resident (C5)",
-            "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+            "value": round(value, 3), "unit": "GB/s", **gpu_fields(world), "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(t, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "vs_baseline": None, "dtype": "u8", "data": "synthetic",
             "config": {"workload": "C5: BCH(1023,983,4) encode + decode with 0-4 bit errors, "
                                    f"{ncw} codewords/GPU (restore copy excluded)",
                        "codewords_per_gpu": ncw, "bytes_per_codeword": row,
@@ -528,7 +547,9 @@ def shard_point(codec, S, steps, warmup, gen):
 
 def timed_pair(enc_fn, dec_fn, steps, warmup, pre=None):
     """Average HIP-event time (ms) of enc_fn and dec_fn on the current stream over `steps` steps;
-    pre() (outside the events) runs before each step."""
+    pre() (outside the events) runs before each step.  The warm-up steps are enqueued right before
+    the timed ones with no host synchronize in between, so the timed calls never start from an idle
+    GPU (an idle gap costs the next ~2 ms a clock ramp: DESIGN.md 5)."""
     import torch
     stream = torch.cuda.current_stream()
     for _ in range(max(1, warmup)):
@@ -536,7 +557,6 @@ def timed_pair(enc_fn, dec_fn, steps, warmup, pre=None):
             pre()
         enc_fn(stream)
         dec_fn(stream)
-    torch.cuda.synchronize()
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
     for e in evs:
         if pre:
@@ -551,12 +571,100 @@ def timed_pair(enc_fn, dec_fn, steps, warmup, pre=None):
             sum(e[1].elapsed_time(e[2]) for e in evs) / steps)
 
 
+def c4_extra(gen, steps=3):
+    """SURVEY 8(d) C4 on the default line: RS(65535,65503), 65 536 codewords (8.6 GB of 16-bit
+    symbols, BASELINE configs[3], rsexercise.C:27-28), each with 12 distinct corrupted symbols of
+    which the last 4 are passed as erasures.  Everything is generated on the device."""
+    import torch
+    import ezrs
+    n, k, ncw = 65535, 65503, 65536
+    c = ezrs.Codec.rs(n, k, device=torch.cuda.current_device())
+    c.reserve(ncw)
+    clean = torch.empty((ncw, n), dtype=torch.int16, device="cuda")
+    for r0 in range(0, ncw, 4096):
+        clean[r0:r0 + 4096] = torch.randint(-32768, 32768, (min(4096, ncw - r0), n), generator=gen,
+                                            device="cuda", dtype=torch.int16)
+    u16 = clean.view(torch.uint16)
+    c.encode(u16, k)
+    units = [s for s in (1, 2, 4, 7, 8, 11, 13, 14, 16, 19, 22, 23, 26, 28, 29, 31) if s % 3 and s % 5]
+    cop = torch.tensor(units, device="cuda")
+    b0 = torch.randint(0, n, (ncw, 1), generator=gen, device="cuda")
+    st = cop[torch.randint(0, len(units), (ncw, 1), generator=gen, device="cuda")]
+    locs = (b0 + torch.arange(12, device="cuda")[None, :] * st) % n     # 12 distinct positions
+    vals = torch.randint(1, 65536, (ncw, 12), generator=gen, device="cuda", dtype=torch.int32).to(torch.int16)
+    master = clean.clone()
+    master.scatter_(1, locs, master.gather(1, locs) ^ vals)
+    eras = locs[:, 8:].to(torch.int32).contiguous()
+    neras = torch.full((ncw,), 4, dtype=torch.int32, device="cuda")
+    work = torch.empty_like(master)
+    res = torch.empty(ncw, dtype=torch.int32, device="cuda")
+    e_ms, d_ms = timed_pair(lambda s_: c.encode(u16, k, stream=s_),
+                            lambda s_: c.decode(work.view(torch.uint16), k, eras=eras, neras=neras,
+                                                result=res, stream=s_),
+                            steps, 1, pre=lambda: work.copy_(master))
+    if not bool((res == 12).all()) or not torch.equal(work, clean):
+        raise SystemExit("C4 extra: decode did not restore the batch")
+    row = 2 * n
+    out = {"codewords": ncw, "encode_ms": round(e_ms, 4), "decode_ms": round(d_ms, 4),
+           "value_gbs": round(ncw * row / ((e_ms + d_ms) * 1e-3) / 1e9, 3),
+           "frac_encode": round(ncw * row / (e_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "frac_decode": round(ncw * (row + 4) / (d_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "traffic": {"ezrs_encode": load_traffic("c4", "ezrs_encode", ncw),
+                       "ezrs_decode": load_traffic("c4", "ezrs_decode", ncw)}}
+    del clean, master, work, res, u16
+    torch.cuda.empty_cache()
+    return out
+
+
+def c5_extra(gen, steps=5, ncw=8 << 20):
+    """SURVEY 8(d) C5 on the default line: BCH(1023,983,4), the config's full 8M-codeword batch on
+    this one GPU (122 data + 5 ECC bytes, bch:196-205,316-331), decode inputs carrying 0..4 random
+    bit errors per codeword (distinct bits).  Everything is generated on the device."""
+    import torch
+    import ezrs
+    L, row = 122, 127
+    c = ezrs.BCH.nkt(1023, 983, 4, device=torch.cuda.current_device())
+    clean = torch.empty((ncw, row), dtype=torch.uint8, device="cuda")
+    for r0 in range(0, ncw, 1 << 20):
+        clean[r0:r0 + (1 << 20)] = torch.randint(0, 256, (min(1 << 20, ncw - r0), row), generator=gen,
+                                                 device="cuda", dtype=torch.int32).to(torch.uint8)
+    c.encode(clean, L)
+    nbits = 8 * L + 40
+    counts = torch.randint(0, 5, (ncw,), generator=gen, device="cuda", dtype=torch.int32)
+    pos = (torch.sort(torch.rand((ncw, 4), generator=gen, device="cuda"), dim=1).values
+           * (nbits - 3)).to(torch.int64) + torch.arange(4, device="cuda")       # distinct bits
+    master = clean.clone()
+    flat = master.view(-1)
+    for j in range(4):
+        r = torch.nonzero(counts > j).squeeze(1)
+        p = pos[r, j]
+        idx = r * row + p // 8
+        flat[idx] = flat[idx] ^ (128 >> (p % 8)).to(torch.uint8)
+    work = torch.empty_like(master)
+    res = torch.empty(ncw, dtype=torch.int32, device="cuda")
+    e_ms, d_ms = timed_pair(lambda s_: c.encode(clean, L, stream=s_),
+                            lambda s_: c.decode(work, L, result=res, stream=s_),
+                            steps, 1, pre=lambda: work.copy_(master))
+    if not torch.equal(res, counts) or not torch.equal(work, clean):
+        raise SystemExit("C5 extra: decode did not restore the batch")
+    out = {"codewords": ncw, "encode_ms": round(e_ms, 4), "decode_ms": round(d_ms, 4),
+           "value_gbs": round(ncw * row / ((e_ms + d_ms) * 1e-3) / 1e9, 3),
+           "frac_encode": round(ncw * row / (e_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "frac_decode": round(ncw * (row + 4) / (d_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "traffic": {"ezbch_encode": load_traffic("c5_8m", "ezbch_encode", ncw),
+                       "ezbch_decode": load_traffic("c5_8m", "ezbch_decode", ncw)}}
+    del clean, master, work, res
+    torch.cuda.empty_cache()
+    return out
+
+
 def c2_extras(codec, args):
     """The north_star / SURVEY 8(d) figures the driver's default run carries beside the headline
     (all timed in the same process, HIP events): shard batches at S = 1 KiB and 1 MiB, C2 at 4M
     codewords (1.07 GB, past the 256 MiB Infinity Cache), the C3 decode (8 errors + 4 erasures per
-    codeword), and the host-memory (PCIe-inclusive) rates, clean and with 1 % of the rows
-    corrupted.  None of these is `value`."""
+    codeword), C4 (RS(65535,65503), 64k codewords), C5 (BCH(1023,983,4), 8M codewords), and the
+    host-memory (PCIe-inclusive) rates, clean and with 1 % of the rows corrupted.  None of these
+    is `value`."""
     import numpy as np
     import torch
     out = {}
@@ -611,6 +719,10 @@ def c2_extras(codec, args):
     log(f"extras: c3 {out['c3']}")
     del clean, master, work, res, locs, vals, eras, neras
     torch.cuda.empty_cache()
+    out["c4"] = c4_extra(gen)
+    log(f"extras: c4 {out['c4']}")
+    out["c5"] = c5_extra(gen)
+    log(f"extras: c5 {out['c5']}")
     # host-memory pipeline (the north_star's PCIe-inclusive rate)
     h = np.random.default_rng(3).integers(0, 256, (ncw, N)).astype(np.uint8)
     hp = torch.from_numpy(h.copy()).pin_memory().numpy()
@@ -696,9 +808,14 @@ def main():
     ap.add_argument("--k", type=int, default=0,
                     help="c2 workload with another RS(255,K) codec (the plane-sliced set: "
                          "NROOTS <= 32); the headline is K = 223")
+    ap.add_argument("--share-gpus", action="store_true",
+                    help="let ranks share GPUs when --gpus exceeds the visible devices (the "
+                         "one-GPU harness test); the line is then marked, never a scaling run")
     ap.add_argument("--harness-check", action="store_true",
                     help="CPU/gloo check of the multi-rank harness (placeholder step, no GPU)")
     args = ap.parse_args()
+    global SHARE_GPUS
+    SHARE_GPUS = args.share_gpus
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(relaunch_distributed(args))
     if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
@@ -762,18 +879,23 @@ def main():
     bad = int((result != 0).sum())
     if bad:
         raise SystemExit(f"rank {rank}: {bad} encoded codewords did not decode clean")
-    # per-call averages for the roofline: K encodes, then K (clean) decodes of the same batch, each
-    # run bracketed by one pair of HIP events on the launch stream
-    def call_ms(fn):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for _ in range(args.steps):
-            fn()
-        e1.record(stream)
-        e1.synchronize()
-        return e0.elapsed_time(e1) / args.steps
-    enc_ms = call_ms(lambda: codec.encode(cw, k, stream=stream))
-    dec_ms = call_ms(lambda: codec.decode(cw, k, result=result, stream=stream))
+    # per-call averages for the roofline: a few untimed steps are enqueued first (the GPU is busy,
+    # not idle, when the first event is recorded), then K encodes and K (clean) decodes of the same
+    # batch back to back, bracketed by three HIP events on the launch stream, one synchronize at
+    # the end
+    for _ in range(3):
+        step()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    ev[0].record(stream)
+    for _ in range(args.steps):
+        codec.encode(cw, k, stream=stream)
+    ev[1].record(stream)
+    for _ in range(args.steps):
+        codec.decode(cw, k, result=result, stream=stream)
+    ev[2].record(stream)
+    ev[2].synchronize()
+    enc_ms = ev[0].elapsed_time(ev[1]) / args.steps
+    dec_ms = ev[1].elapsed_time(ev[2]) / args.steps
 
     total_cw = ncw * world * args.steps
     value = total_cw * n / elapsed / 1e9
@@ -818,9 +940,9 @@ def main():
 
     if rank == 0:
         line = {"metric": f"RS({n},{k}) encode+decode GB/s device-resident",
-                "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+                "value": round(value, 3), "unit": "GB/s", **gpu_fields(world), "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-                "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                "higher_is_better": True, "vs_baseline": None,
                 "dtype": "u8", "data": "synthetic",
                 "config": {"workload": f"{args.workload.upper()}: RS({n},{k}) encode + clean decode, "
                                        f"{ncw} codewords/GPU",

@@ -14,50 +14,48 @@
 #                per (pad, load) class (exercise.c:136-138): rstest.c's Tab asks for up to 100000
 #                single-codeword round trips per class, hours of PCIe round trips through a GPU
 #
-# The tarball is unpacked (headers only are used) into a scratch directory with the reference's
-# int-symbol patch applied, exactly as phil-karn/GNUmakefile:43-52 prepares it.  Nothing from the
-# reference is copied into the repository.
+# The tarball is unpacked (headers only are used) into a temporary directory outside the repository,
+# with the reference's int-symbol patch applied exactly as phil-karn/GNUmakefile:43-52 prepares it,
+# and the directory is deleted when the recipe ends: no reference source stays under tests/ or
+# travels to the GPU box.  Nothing from the reference is copied into the repository.
 REFERENCE ?= /root/reference
 HERE      := $(dir $(abspath $(lastword $(MAKEFILE_LIST))))
 ROOT      := $(abspath $(HERE)../..)
 OUT       := $(HERE)_bin
 LIB       := $(ROOT)/ezpwd-reed-solomon_amd/lib
 KARNLIB   := $(ROOT)/oracle/_ref
-FECDIR    := $(OUT)/.fec
 CXXF      := -std=c++17 -O2 -w -I$(ROOT)/include -I$(REFERENCE)/c++ -I$(REFERENCE)
-KARNF     := -I$(REFERENCE)/phil-karn -I$(FECDIR)
+TGZ       := $(REFERENCE)/phil-karn/fec-3.0.1.tar.gz
+KEX       := $(REFERENCE)/phil-karn/exercise.c
 
 .PHONY: all
-all: $(OUT)/rsexercise $(OUT)/rsvalidate $(OUT)/rsspeed $(OUT)/rstest
-
-$(FECDIR)/fec/fec.h: $(REFERENCE)/phil-karn/fec-3.0.1.tar.gz
-	rm -rf $(FECDIR) && mkdir -p $(FECDIR)
-	tar xzf $< -C $(FECDIR)
-	cd $(FECDIR)/fec-3.0.1 && for p in $(REFERENCE)/phil-karn/fec-3.0.1*.patch; do patch -s -p1 < $$p; done
-	ln -sfn fec-3.0.1 $(FECDIR)/fec
-	touch $@
+all: $(OUT)/rsexercise $(OUT)/.karn_stamp
 
 $(OUT)/rsexercise: $(REFERENCE)/rsexercise.C $(REFERENCE)/exercise.H $(ROOT)/include/ezpwd_amd/rs
 	@mkdir -p $(OUT)
 	g++ $(CXXF) -o $@ $< -L$(LIB) -lezrs_hip -Wl,-rpath,$(LIB)
 
-$(OUT)/rsvalidate: $(REFERENCE)/rsvalidate.C $(ROOT)/include/ezpwd_amd/rs $(FECDIR)/fec/fec.h
+# rsvalidate, rsspeed and rstest: the programs that need libfec's headers, built in one recipe around
+# one temporary unpack of the tarball
+$(OUT)/.karn_stamp: $(REFERENCE)/rsvalidate.C $(REFERENCE)/rsspeed.C $(REFERENCE)/phil-karn/rstest.c $(KEX) \
+                    $(TGZ) $(ROOT)/include/ezpwd_amd/rs $(LIB)/libezrs_fec.so $(HERE)harness.mk
 	@mkdir -p $(OUT)
-	g++ $(CXXF) $(KARNF) -o $@ $< -L$(LIB) -lezrs_hip -L$(KARNLIB) -lkarn -Wl,-rpath,$(LIB) -Wl,-rpath,$(KARNLIB)
-
-$(OUT)/rsspeed: $(REFERENCE)/rsspeed.C $(ROOT)/include/ezpwd_amd/rs $(FECDIR)/fec/fec.h
-	@mkdir -p $(OUT)
-	g++ $(CXXF) $(KARNF) -o $@ $< -L$(LIB) -lezrs_hip -L$(KARNLIB) -lkarn -Wl,-rpath,$(LIB) -Wl,-rpath,$(KARNLIB)
-
-KEX := $(REFERENCE)/phil-karn/exercise.c
-KCF := -O2 -w -I$(FECDIR)/fec-3.0.1 $(KARNF)
-KXF := $(KCF) -DDEBUG=1
-$(OUT)/rstest: $(REFERENCE)/phil-karn/rstest.c $(KEX) $(FECDIR)/fec/fec.h $(LIB)/libezrs_fec.so
-	@mkdir -p $(OUT)/.o
-	gcc $(KCF) -c -o $(OUT)/.o/rstest.o $(REFERENCE)/phil-karn/rstest.c
-	gcc $(KXF) -c -o $(OUT)/.o/exercise_char.o $(KEX)
-	gcc $(KXF) -DBIGSYM -c -o $(OUT)/.o/exercise_int.o $(KEX)
-	gcc $(KXF) -DFIXED -c -o $(OUT)/.o/exercise_8.o $(KEX)
-	gcc $(KXF) -DCCSDS -c -o $(OUT)/.o/exercise_ccsds.o $(KEX)
-	g++ -o $@ $(OUT)/.o/rstest.o $(OUT)/.o/exercise_char.o $(OUT)/.o/exercise_int.o \
-	    $(OUT)/.o/exercise_8.o $(OUT)/.o/exercise_ccsds.o -L$(LIB) -lezrs_fec -lezrs_hip -Wl,-rpath,$(LIB)
+	@rm -rf $(OUT)/.fec $(OUT)/.o
+	T=$$(mktemp -d /tmp/ezrs_fec.XXXXXX) && ( set -e; \
+	  tar xzf $(TGZ) -C $$T; \
+	  cd $$T/fec-3.0.1 && for p in $(REFERENCE)/phil-karn/fec-3.0.1*.patch; do patch -s -p1 < $$p; done; \
+	  ln -sfn fec-3.0.1 $$T/fec; \
+	  KF="-I$(REFERENCE)/phil-karn -I$$T"; \
+	  g++ $(CXXF) $$KF -o $(OUT)/rsvalidate $(REFERENCE)/rsvalidate.C -L$(LIB) -lezrs_hip -L$(KARNLIB) -lkarn \
+	      -Wl,-rpath,$(LIB) -Wl,-rpath,$(KARNLIB); \
+	  g++ $(CXXF) $$KF -o $(OUT)/rsspeed $(REFERENCE)/rsspeed.C -L$(LIB) -lezrs_hip -L$(KARNLIB) -lkarn \
+	      -Wl,-rpath,$(LIB) -Wl,-rpath,$(KARNLIB); \
+	  KC="-O2 -w -I$$T/fec-3.0.1 $$KF"; \
+	  gcc $$KC -c -o $$T/rstest.o $(REFERENCE)/phil-karn/rstest.c; \
+	  gcc $$KC -DDEBUG=1 -c -o $$T/ex_char.o $(KEX); \
+	  gcc $$KC -DDEBUG=1 -DBIGSYM -c -o $$T/ex_int.o $(KEX); \
+	  gcc $$KC -DDEBUG=1 -DFIXED -c -o $$T/ex_8.o $(KEX); \
+	  gcc $$KC -DDEBUG=1 -DCCSDS -c -o $$T/ex_ccsds.o $(KEX); \
+	  g++ -o $(OUT)/rstest $$T/rstest.o $$T/ex_char.o $$T/ex_int.o $$T/ex_8.o $$T/ex_ccsds.o \
+	      -L$(LIB) -lezrs_fec -lezrs_hip -Wl,-rpath,$(LIB) ); rc=$$?; rm -rf $$T; exit $$rc
+	touch $@

@@ -8,7 +8,13 @@ built by __graft_entry__.build()), run on the GPU:
               decode cross-checked against Phil Karn's CPU libfec; zero failures (rsvalidate.C:382-385)
   rsspeed     rsspeed.C: the same pairing on 11 codecs, asserting identical corrections
   rstest      phil-karn/rstest.c + exercise.c linked against libezrs_fec.so: Karn's ABI over the
-              engine; every Tab row prints OK and the run ends "All codec tests passed!"
+              engine; every Tab row prints OK and the run ends "All codec tests passed!".
+              exercise.c is built with the reference's own -DDEBUG=1 knob (exercise.c:136-138),
+              which runs 10 trials per (pad, load) class instead of rstest.c's Tab counts (up to
+              100 000): each trial is a single-codeword call, a PCIe round trip through the GPU.
+              This run is therefore a thin check of the ABI; the bulk of the Karn-mode coverage is
+              the batch-form fixture test tests/test_karn_abi_gpu.py (libfec's own outputs over
+              shortened codewords, pad erasures, loads to 1.6x the parity, every Tab symbol size).
 """
 import os
 import subprocess
