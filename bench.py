@@ -792,6 +792,8 @@ def main():
                          "idle GPU -- the synchronize before it -- and carries a fixed ~2 ms while "
                          "the clocks come back up; r04v: 100 steps 1371 GB/s, 400 1468, 1000 1496)")
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--spinup", type=float, default=0.5,
+                    help="seconds of untimed device spin-up (whole steps) before the counted warm-up")
     ap.add_argument("--ncw", type=int, default=1 << 20, help="codewords per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=3.0,
@@ -856,6 +858,16 @@ def main():
         codec.encode(cw, k, stream=stream)
         codec.decode(cw, k, result=result, stream=stream)
 
+    # untimed device spin-up before the W counted warm-up steps: r05a probe (tools/step_probe.py)
+    # -- in a fresh process the first ~50 steps run 10-25 % slower (0.23 -> 0.195 -> 0.18 ms) while
+    # the GPU settles, which a 20-step timed region after 5 warm-up steps would carry; the spin-up is
+    # reported on the line ("spinup_s")
+    t_spin = time.perf_counter()
+    while time.perf_counter() - t_spin < args.spinup:
+        for _ in range(25):
+            step()
+        torch.cuda.synchronize()
+    spinup_s = time.perf_counter() - t_spin
     for _ in range(args.warmup):
         step()
 
@@ -942,7 +954,7 @@ def main():
         line = {"metric": f"RS({n},{k}) encode+decode GB/s device-resident",
                 "value": round(value, 3), "unit": "GB/s", **gpu_fields(world), "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-                "higher_is_better": True, "vs_baseline": None,
+                "higher_is_better": True, "vs_baseline": None, "spinup_s": round(spinup_s, 3),
                 "dtype": "u8", "data": "synthetic",
                 "config": {"workload": f"{args.workload.upper()}: RS({n},{k}) encode + clean decode, "
                                        f"{ncw} codewords/GPU",

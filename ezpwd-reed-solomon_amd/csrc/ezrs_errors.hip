@@ -30,6 +30,12 @@ namespace ezrs {
 namespace {
 
 constexpr int32_t kSentinel = INT32_MIN;
+#ifndef EZRS_ERR_STOP
+#define EZRS_ERR_STOP 0                 // timing ablations (variant builds only): see decode_lane
+#endif
+#ifndef EZRS_ERR_NOCACHE
+#define EZRS_ERR_NOCACHE 0
+#endif
 
 constexpr int kSpan = 256;              // result slots screened per wavefront
 constexpr int kWaves = 16;              // wavefronts per workgroup (one workgroup per CU)
@@ -84,7 +90,8 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
     // erasure positions (1383-1387): loaded four at a time where the row allows (all loads issued
     // before the first use) and kept as bytes in this lane's Chien root column, free until the
     // search, for the erasure locator
-    if (no_eras > 0) {
+    bool eras_bad = false;                    // Karn mode: an erasure outside the frame, reported after
+    if (no_eras > 0) {                        // the zero-syndrome return as libfec does
         unsigned bad = 0;
         uint8_t *ep = W.root + lane;
         if ((reinterpret_cast<uintptr_t>(eras) & 15) == 0 && ((no_eras + 3) & ~3u) <= eras_cap) {
@@ -112,7 +119,8 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
                 ep[i * 64] = (uint8_t)x;
             }
         }
-        if (bad) return -1;
+        if (bad && !karn) return -1;
+        if (bad) eras_bad = true;
     }
     const unsigned pad = LOAD - len;
     const unsigned epad = karn ? 0u : pad;    // frame offset of an erasure position
@@ -132,6 +140,7 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
         for (int k = 32; k < kSrows; ++k) S(k) = kZ;
     }
     if (!syn_error) return 0;
+    if (eras_bad) return -1;                  // (Karn mode only: undefined in libfec, -1 here)
 
     // erasure locator (1436-1450): lambda in polynomial form, lam[0] == 1
     unsigned lam[33];
@@ -157,6 +166,9 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
     unsigned b[33], l[33];
 #pragma unroll
     for (int i = 0; i <= 32; ++i) b[i] = i == 0 ? 0u : gi(L, lam[i]);
+#if EZRS_ERR_STOP == 4                  // timing ablation: syndromes and erasure locator only
+    { unsigned x = 0; for (int i = 0; i <= 32; ++i) x ^= lam[i]; return (int)(x & 1); }
+#endif
 
     // Berlekamp-Massey (1507-1546).  Before step r, deg lambda <= el and deg B <= r - 1 - el +
     // no_eras (the reference's length rule keeps both; checked exhaustively against a model), so
@@ -167,6 +179,9 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
 #pragma unroll
     for (int i = 0; i <= 32; ++i) l[i] = i == 0 ? 0u : kZ;
     unsigned el = no_eras;
+    // l[1 .. lhi] hold log lambda for this lane (reset when its lambda changes): an iteration with a
+    // zero discrepancy leaves lambda alone, and the next one reuses the logs
+    unsigned lhi = 0;
     for (unsigned r = no_eras + 1; r <= NR; ++r) {
         const int sb = 32 - (int)r;           // row of S_{r-1}; S_{r-1-i} at row sb + i
         const unsigned dmax = min(r - 1, el), umax = max(el, r + no_eras - el);
@@ -174,13 +189,15 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
 #pragma unroll
         for (int i0 = 0; i0 <= 32; i0 += 4) {
             if ((unsigned)i0 <= dmax) {
+                if (EZRS_ERR_NOCACHE || (unsigned)i0 + 3u > lhi) {
 #pragma unroll
-                for (int i = i0; i < i0 + 4 && i <= 32; ++i) {
-                    l[i] = i == 0 ? 0u : gi(L, lam[i]);
-                    if (i < 32) discr ^= gp(L, (l[i] + S(sb + i)));
+                    for (int i = i0; i < i0 + 4 && i <= 32; ++i) l[i] = i == 0 ? 0u : gi(L, lam[i]);
                 }
+#pragma unroll
+                for (int i = i0; i < i0 + 4 && i < 32; ++i) discr ^= gp(L, (l[i] + S(sb + i)));
             }
         }
+        lhi = max(lhi, (dmax & ~3u) + 3u);
         const unsigned dl = gi(L, discr);
         const bool upd = dl < 510u && 2 * el <= r + no_eras - 1;
         const unsigned ndl = 255u - dl;
@@ -198,8 +215,12 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
                 }
             }
         }
+        if (dl < 510u) lhi = 0;               // this lane's lambda changed
         el = upd ? r + no_eras - el : el;
     }
+#if EZRS_ERR_STOP == 1                  // timing ablation: up to Berlekamp-Massey
+    { unsigned x = 0; for (int i = 0; i <= 32; ++i) x ^= lam[i]; return (int)(x & 1); }
+#endif
 
     // lambda to index form, its degree (1549-1553)
     unsigned deg = 0;
@@ -244,6 +265,9 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
         }
     }
     if ((int)deg != count || (deg == 0 && !karn)) count = -1;                // 1577-1595 (Karn: 0)
+#if EZRS_ERR_STOP == 2                  // timing ablation: up to the Chien search
+    return count;
+#endif
 
     if (count > 0) {
         // Omega = S * lambda mod x^(deg lambda), index form (1596-1604)
@@ -290,7 +314,10 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
             if (num1 != 0) {
                 const unsigned loc = (rj * c.iprim + 254u) % 255u;
                 if (loc < pad) {
-                    if (karn) continue;
+                    if (karn) {                       // skipped, as libfec does: no correction
+                        if (corr_out) corr_out[j] = 0;
+                        continue;
+                    }
                     count = -1;
                     break;
                 }
@@ -321,6 +348,9 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
                 if (corr_out) corr_out[j] = (uint8_t)cv;
             }
         }
+#if EZRS_ERR_STOP == 3                  // timing ablation: no corrections applied
+        return (int)nrec;
+#endif
         for (unsigned g0 = 0; g0 < nrec; g0 += 8) {
             uint8_t *at[8];
             unsigned v[8], dlt[8];

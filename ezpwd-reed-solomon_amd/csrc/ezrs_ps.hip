@@ -39,6 +39,12 @@
 
 #include <atomic>
 #include "gen/ezrs_ps_tables.inc"
+#ifdef EZRS_PS_ONLY_223
+// timing-experiment builds only (tools/build_variant.sh): the plane-sliced path for RS(255,223)
+// alone (every other codec takes the generic kernels), so a variant compiles in about a minute
+#undef EZRS_PS_CODEC_LIST
+#define EZRS_PS_CODEC_LIST(X) X(RS_255_223)
+#endif
 
 namespace ezrs {
 namespace ps {
@@ -62,9 +68,17 @@ __device__ unsigned long long g_pt_stamps[16][8][8][8];
     __lane_id() == 0) g_pt_stamps[blockIdx.x][pt_w][pt_it][ph] = __builtin_amdgcn_s_memtime(); \
     __builtin_amdgcn_sched_barrier(0); } while (0)
 // tools/micro/pq_stamps.hip: the same for the 4-wave kernel, [wg][wave][tile][phase]
-__device__ unsigned long long g_pq_stamps[16][4][8][8];
-#define PQ_STAMP(ph) do { __builtin_amdgcn_sched_barrier(0); if (blockIdx.x < 16 && pq_it < 8 && \
+__device__ unsigned long long g_pq_stamps[512][4][9][8];
+__device__ unsigned long long g_pq_rt[512][4];             // wave 0: realtime + memtime at start / end
+__device__ unsigned g_pq_hw[512][2];                       // wave 0: HW_ID, XCC_ID
+#define PQ_STAMP(ph) do { __builtin_amdgcn_sched_barrier(0); if (blockIdx.x < 512 && pq_it < 9 && \
     __lane_id() == 0) g_pq_stamps[blockIdx.x][W][pq_it][ph] = __builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0); } while (0)
+#define PQ_RT(i) do { __builtin_amdgcn_sched_barrier(0); if (blockIdx.x < 512 && W == 0 && __lane_id() == 0) { \
+    g_pq_rt[blockIdx.x][2 * (i)] = __builtin_amdgcn_s_memrealtime(); \
+    g_pq_rt[blockIdx.x][2 * (i) + 1] = __builtin_amdgcn_s_memtime(); \
+    if ((i) == 0) { g_pq_hw[blockIdx.x][0] = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11)); \
+                    g_pq_hw[blockIdx.x][1] = __builtin_amdgcn_s_getreg(20 | (0 << 6) | (31 << 11)); } } \
     __builtin_amdgcn_sched_barrier(0); } while (0)
 // tools/micro/par_stamps.hip: the parity kernel's phases, [block][wave][phase]
 __device__ unsigned long long g_par_stamps[64][8][8];
@@ -79,6 +93,7 @@ __device__ unsigned g_par_hw[4096];                        // HW_ID of wave 0
 #else
 #define PT_STAMP(ph) do { } while (0)
 #define PQ_STAMP(ph) do { } while (0)
+#define PQ_RT(i) do { } while (0)
 #define PAR_STAMP(ph) do { } while (0)
 #endif
 
@@ -649,6 +664,87 @@ k_pt_lin(PsArgs a) {
 
 } // namespace pt
 
+namespace xpk {
+using pt::u32x4;
+constexpr int kXArea = 32768;                 // at most 16 items of 2 KiB per sub-round
+// Packed exchange (k_pq_lin, k_pq2): window [J0, J0 + 4) of sub-round S of the generated plan (XS / XV),
+// the items of all waves of the window packed one after the other (2 KiB each) in an area of at most
+// kXArea bytes; a window no wave uses is skipped.
+template <class C, int S, int J0, int W>
+constexpr int xbase() {
+    int n = 0;
+    for (int w = 0; w < W; ++w)
+        for (int j = J0; j < J0 + 4 && j < C::XCAP; ++j) n += C::XS[w][S][j] >= 0;
+    return n;
+}
+// index of item j among wave W's sent items of the window
+template <class C, int S, int J0, int W>
+constexpr int xidx(int j) {
+    int n = 0;
+    for (int i = J0; i < j; ++i) n += C::XS[W][S][i] >= 0;
+    return n;
+}
+template <class C, int S, int J0>
+constexpr int xtotal() {
+    int n = 0;
+    for (int w = 0; w < 4; ++w)
+        for (int j = J0; j < J0 + 4 && j < C::XCAP; ++j) n += C::XS[w][S][j] >= 0;
+    return n;
+}
+template <class C, int S, int J0, int W, int J = J0>
+__device__ __forceinline__ void xsend(uint32_t (&V)[C::NI][8], uint32_t lx) {
+    if constexpr (J < J0 + 4 && J < C::XCAP) {
+        constexpr int it = C::XS[W][S][J];
+        if constexpr (it >= 0) {
+            constexpr int slot = xbase<C, S, J0, W>() + xidx<C, S, J0, W>(J);
+            const u32x4 w0 = {V[it][0], V[it][1], V[it][2], V[it][3]};
+            const u32x4 w1 = {V[it][4], V[it][5], V[it][6], V[it][7]};
+            asm volatile("ds_write_b128 %0, %1 offset:%3\n\t"
+                         "ds_write_b128 %0, %2 offset:%4"
+                         :: "v"(lx), "v"(w0), "v"(w1), "n"(slot * 2048), "n"(slot * 2048 + 1024) : "memory");
+        }
+        xsend<C, S, J0, W, J + 1>(V, lx);
+    }
+}
+template <class C, int S, int J0, int W, int PW, int J = J0>
+__device__ __forceinline__ void xrecv(uint32_t (&V)[C::NI][8], uint32_t lx) {
+    if constexpr (J < J0 + 4 && J < C::XCAP) {
+        constexpr int it = C::XV[W][S][J];
+        if constexpr (it >= 0) {
+            static_assert(C::XS[PW][S][J] >= 0, "partner sends what this wave adds");
+            constexpr int slot = xbase<C, S, J0, PW>() + xidx<C, S, J0, PW>(J);
+            u32x4 b[2];
+            asm volatile("ds_read_b128 %0, %2 offset:%3\n\t"
+                         "ds_read_b128 %1, %2 offset:%4\n\t"
+                         "s_waitcnt lgkmcnt(0)"
+                         : "=&v"(b[0]), "=&v"(b[1]) : "v"(lx), "n"(slot * 2048), "n"(slot * 2048 + 1024) : "memory");
+            V[it][0] ^= b[0].x; V[it][1] ^= b[0].y; V[it][2] ^= b[0].z; V[it][3] ^= b[0].w;
+            V[it][4] ^= b[1].x; V[it][5] ^= b[1].y; V[it][6] ^= b[1].z; V[it][7] ^= b[1].w;
+        }
+        xrecv<C, S, J0, W, PW, J + 1>(V, lx);
+    }
+}
+template <class C, int W, int S = 0, int J0 = 0>
+__device__ __forceinline__ void exchange(uint32_t (&V)[C::NI][8], uint32_t lx) {
+    if constexpr (S < C::NSUB) {
+        if constexpr (J0 >= C::XCAP) {
+            exchange<C, W, S + 1, 0>(V, lx);
+        } else {
+            if constexpr (xtotal<C, S, J0>() > 0) {
+                static_assert(xtotal<C, S, J0>() * 2048 <= kXArea, "sub-round fits the area");
+                xsend<C, S, J0, W>(V, lx);
+                pt::wait_lgkm();
+                pt::barrier();
+                xrecv<C, S, J0, W, W ^ (1 << C::XR[S])>(V, lx);
+                pt::barrier();                               // read before the area is reused
+            }
+            exchange<C, W, S, J0 + 4>(V, lx);
+        }
+    }
+}
+
+} // namespace xpk
+
 // ---- 4-wave tile kernel k_pq_lin (PQ_<codec>, codegen gen_pq) -----------------------------------
 // One 256-thread workgroup (4 waves) per 256-codeword tile, two workgroups per CU (80 KiB LDS
 // each), up to 256 VGPRs (2 waves per SIMD).  Wave W evaluates EVERY coset leader (NI x 8 state
@@ -671,6 +767,11 @@ constexpr int kLds = 81920;                   // 80 KiB: two workgroups per CU
 constexpr int kFlags = kGuard + kImage;       // decode flags [4][64] after the image
 constexpr int kTab = kFlags + 1024;           // shard batches: per-row image offset and pad [256]
 static_assert(kTab + 1024 <= kLds, "pq tile kernel LDS");
+// the packed exchange's area at the top of the LDS (over the image's last 16 KiB and the flags and
+// row table, whose uses do not overlap the exchange); the DMA instructions below it (kEarly) go out
+// before the exchange
+constexpr int kXBase = kLds - xpk::kXArea;
+constexpr int kEarly = (kXBase - kGuard) / 1024;
 
 // Raw dwords of rows 4l + k at one 16-position piece (4-byte aligned reads, aligned afterwards).
 struct Raw {
@@ -874,11 +975,13 @@ __device__ __forceinline__ void exchange(uint32_t (&V)[C::NI][8], uint32_t lx) {
     }
 }
 
-__device__ __forceinline__ void issue_tile(uint32_t lbuf, pw_rsrc_t rsrc, uint32_t toff, uint32_t tile_bytes, int w) {
+// instructions [i0, i1) of the tile's DMA, wave w taking every fourth
+__device__ __forceinline__ void issue_tile(uint32_t lbuf, pw_rsrc_t rsrc, uint32_t toff, uint32_t tile_bytes, int w,
+                                           uint32_t i0 = 0, uint32_t i1 = 64) {
 #ifdef EZRS_PQ_ABL_NODMA
     return;                                                  // timing-only builds (pq_stamps)
 #endif
-    const uint32_t ninstr = (tile_bytes + 1023) >> 10;
+    const uint32_t ninstr = min((tile_bytes + 1023) >> 10, i1);
     const uint32_t lo16 = 16u * pt::fresh();
 #ifdef EZRS_PQ_DMA_M0X4
     // wave w: pieces 16w .. 16w+15, four per M0 value (the instruction offset steps both the
@@ -900,7 +1003,7 @@ __device__ __forceinline__ void issue_tile(uint32_t lbuf, pw_rsrc_t rsrc, uint32
                              :: "s"(lbuf + kGuard + j * 1024u), "v"(toff + j * 1024u + lo16), "s"(rsrc) : "memory", "m0");
     }
 #else
-    for (uint32_t i = w; i < ninstr; i += kWaves)
+    for (uint32_t i = i0 + (uint32_t)((w - (int)i0) & 3); i < ninstr; i += kWaves)
         asm volatile("s_mov_b32 m0, %0\n\t"
                      "s_nop 0\n\t"
                      "buffer_load_dwordx4 %1, %2, 0 offen lds"
@@ -939,10 +1042,19 @@ __device__ __forceinline__ void wave_tail(uint32_t (&V)[C::NI][8], const PsArgs 
                                           uint32_t noff, uint32_t nbytes, pw_rsrc_t rsrc, pw_rsrc_t rout,
                                           pw_rsrc_t rws, int pq_it = 0) {
     (void)pq_it;
+#ifdef EZRS_PQ_EARLYDMA
+    // (measured and dropped, opt-in: decode 0.072 vs 0.066 ms) the next tile's first kEarly KiB land in the image below the exchange area as soon as the
+    // main loop has consumed it; the rest once the exchange (at the top of the LDS) is done
+    if (noff != kOob) issue_tile(lbuf, rsrc, noff, nbytes, W, 0, kEarly);
+    xpk::exchange<C, W>(V, lbuf + (uint32_t)kXBase + 16u * pt::fresh());
+    PQ_STAMP(4);
+    if (noff != kOob) issue_tile(lbuf, rsrc, noff, nbytes, W, kEarly, 64);
+#else
     exchange<C, W, 0>(V, lbuf + 16u * pt::fresh());
     PQ_STAMP(4);
 #if !defined(EZRS_PQ_DMA_LATE) && !defined(EZRS_PQ_DMA_SPREAD)
     if (noff != kOob) issue_tile(lbuf, rsrc, noff, nbytes, W);
+#endif
 #endif
     uint32_t T[C::NOWN][8];
 #pragma unroll
@@ -1056,6 +1168,7 @@ __device__ __forceinline__ void pq_run(const PsArgs &a, uint8_t *lds) {
         return off;
     };
     uint32_t tile = blockIdx.x;
+    PQ_RT(0);
     uint32_t tbytes, toff = tile < a.ntiles ? tile_range(tile, tbytes) : 0u;
     if (tile < a.ntiles) issue_tile(lbuf, rsrc, toff, tbytes, W);
     int pq_it = 0;
@@ -1115,6 +1228,7 @@ __device__ __forceinline__ void pq_run(const PsArgs &a, uint8_t *lds) {
         tbytes = nbytes;
     }
     pt::wait_vm<0>();                                        // no DMA may land after the exit
+    PQ_RT(1);
 }
 
 template <class C, bool ENC, bool SH, bool LO0>
@@ -1132,6 +1246,318 @@ k_pq_lin(PsArgs a) {
 }
 
 } // namespace pq
+
+// ---- double-buffered 4-wave tile kernel k_pq2 (PQ_<codec> networks, full-length packed rows) ------
+// The tile's 256 rows are taken in two position chunks, 0..127 and 128..254, each with its own 36 KiB
+// LDS slot: the next tile's chunk 0 is DMA'd into slot 0 while this tile's chunk 1 is processed (its
+// issues spread through that main loop), and its chunk 1 into slot 1 once this tile's exchange has
+// released the slot (spread through the fold).  k_pq_lin has one 64 KiB image per workgroup, so its
+// next tile's DMA could only start after the exchange; r05d stamps on clean data: of 17.0 k ticks
+// per tile, 5.4 k were the wave waiting for that DMA.
+//   * A chunk slot holds 9 aligned 16-byte pieces per row (a row's chunk spans at most 143 bytes
+//     with its 16-byte phase): the pieces are gathered by LDS-DMA with per-lane source addresses;
+//     every instruction's 1 KiB covers whole rows' pieces (about 7 rows), so a line is fetched
+//     once per chunk.
+//   * Row r's pieces sit at slot position sigma(r) = (l >> 2) + 16 (l & 3) + 64 k for r = 4 l + k:
+//     lane l reads its rows 4l + k (the codeword mapping of k_pq_lin, so every workspace layout is
+//     unchanged) at dword addresses 36 sigma + phase / 4, which fall in 32 distinct banks per half
+//     wave for each k.
+//   * The exchange runs in slot 1 in sub-rounds of at most 32 KiB (items packed over the waves).
+// Used for plain batches of full-length RS(255,223) rows at pitch 255 with a 16-byte aligned base;
+// every other geometry keeps k_pq_lin.
+namespace pq2 {
+
+using pt::kOob;
+using pt::u32x2;
+using pt::u32x4;
+using pq::Raw;
+constexpr int kThreads = 256;
+constexpr int kWaves = 4;
+constexpr int kPitch = 144;                   // bytes per row in a chunk slot: 9 pieces
+constexpr int kSlot = 256 * kPitch;           // 36 KiB = 36 DMA instructions of 1 KiB
+constexpr int kInstrW = kSlot / 1024 / kWaves;    // 9 per wave per chunk
+constexpr int kFlags = 2 * kSlot;             // decode flags [4][64]
+constexpr int kLds = kFlags + 1024;
+static_assert(kLds <= 81920, "two workgroups per CU");
+static_assert(kSlot % (1024 * kWaves) == 0, "whole DMA instructions per wave");
+
+__host__ __device__ constexpr uint32_t slot_pos(uint32_t r) {
+    return ((r >> 2) >> 2) + 16u * ((r >> 2) & 3u) + 64u * (r & 3u);
+}
+__host__ __device__ constexpr uint32_t row_of(uint32_t sig) {
+    return 4u * (4u * (sig & 15u) + ((sig & 63u) >> 4)) + (sig >> 6);
+}
+static_assert(row_of(slot_pos(137)) == 137 && row_of(slot_pos(255)) == 255 && row_of(slot_pos(4)) == 4, "slot map");
+
+// wave W's DMA source offsets (from the tile's first byte) for its pieces n = 0..8 of a chunk:
+// instruction j = W + 4n, lane i -> slot piece s = 64 j + i -> row row_of(s / 9), piece s % 9
+template <int W>
+__device__ __forceinline__ void dma_offsets(uint32_t (&off)[kInstrW]) {
+    const uint32_t lane = pt::fresh();
+#pragma unroll
+    for (int n = 0; n < kInstrW; ++n) {
+        const uint32_t s = 64u * (uint32_t)(W + 4 * n) + lane, sig = s / 9u, pc = s - 9u * sig;
+        off[n] = ((255u * row_of(sig)) & ~15u) + 16u * pc;
+    }
+}
+__device__ __forceinline__ void dma_piece(uint32_t m0, uint32_t voff, pw_rsrc_t rsrc) {
+    asm volatile("s_mov_b32 m0, %0\n\t"
+                 "s_nop 0\n\t"
+                 "buffer_load_dwordx4 %1, %2, 0 offen lds"
+                 :: "s"(m0), "v"(voff), "s"(rsrc) : "memory", "m0");
+}
+// wave W's pieces N0 .. N1-1 of chunk c of the tile whose first byte is at buffer offset tb
+template <int W, int N0, int N1>
+__device__ __forceinline__ void dma_run(const uint32_t (&off)[kInstrW], uint32_t lslot, uint32_t tb, pw_rsrc_t rsrc) {
+#pragma unroll
+    for (int n = N0; n < N1 && n < kInstrW; ++n) dma_piece(lslot + 1024u * (uint32_t)(W + 4 * n), off[n] + tb, rsrc);
+}
+
+// lane l's row k: dword-aligned LDS address of its chunk's position 0 (at4) and the byte phase
+// (at & 3, the v_alignbyte shift)
+__device__ __forceinline__ void row_addrs(uint32_t (&at)[4], uint32_t (&at4)[4], uint32_t lslot) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t r = 4u * pt::fresh() + k, ph = (0u - r) & 15u;   // (255 r) mod 16
+        at[k] = lslot + (uint32_t)kPitch * slot_pos(r) + ph;
+        at4[k] = at[k] & ~3u;
+    }
+}
+
+// Piece I of a run: blocks B, B+1 (absolute; positions from chunk c's first at OFF = 8 B - 128 c),
+// the next piece's reads in flight.  H(b) runs after block b (DMA issues).
+template <class C, int HI, int CH, int B, int B1, bool F, class H>
+__device__ __forceinline__ void piece(uint32_t (&V)[C::NI][8], Raw &cur, const uint32_t (&at)[4],
+                                      const uint32_t (&at4)[4], H &&hook) {
+    if constexpr (B < B1) {
+        pq::wait_raw(cur);
+        Raw nxt;
+        if constexpr (B + 2 < B1) pq::issue_piece<8 * (B + 2) - 128 * CH, (B + 3 >= B1)>(nxt, at4);
+        __builtin_amdgcn_sched_barrier(0);
+        u32x4 R[4];
+        pq::align_rows<false>(R, cur, at, 8 * B, 0, 0u);
+        uint32_t X[8];
+        {
+            const uint32_t c0[4] = {R[0].x, R[1].x, R[2].x, R[3].x};
+            const uint32_t c1[4] = {R[0].y, R[1].y, R[2].y, R[3].y};
+            transpose4x4(c0, X);
+            transpose4x4(c1, X + 4);
+        }
+        pq::block8<C, HI, B, F, true>(V, X, 0);
+        hook(std::integral_constant<int, B>{});
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (B + 1 < B1) {
+            const uint32_t c2[4] = {R[0].z, R[1].z, R[2].z, R[3].z};
+            const uint32_t c3[4] = {R[0].w, R[1].w, R[2].w, R[3].w};
+            transpose4x4(c2, X);
+            transpose4x4(c3, X + 4);
+            pq::block8<C, HI, B + 1, false, true>(V, X, 0);
+            hook(std::integral_constant<int, B + 1>{});
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (B + 2 < B1) piece<C, HI, CH, B + 2, B1, false, H>(V, nxt, at, at4, hook);
+    }
+}
+template <class C, int HI, int CH, int B0, int B1, bool F, class H>
+__device__ __forceinline__ void run(uint32_t (&V)[C::NI][8], uint32_t lslot, H &&hook) {
+    if constexpr (B0 < B1) {
+        uint32_t at[4], at4[4];
+        row_addrs(at, at4, lslot);
+        Raw cur;
+        pq::issue_piece<8 * B0 - 128 * CH, (B0 + 1 >= B1)>(cur, at4);
+        piece<C, HI, CH, B0, B1, F>(V, cur, at, at4, hook);
+    }
+}
+
+// wave W's blocks in chunk CH: decode 4 per wave per chunk (chunk 1's last block masks position
+// 255); encode chunk 1 holds the data blocks 16 .. 27, 3 per wave
+template <bool ENC, int W, int CH>
+struct Blocks {
+    static constexpr int PER = CH == 0 ? 4 : (ENC ? 3 : 4);
+    static constexpr int B0 = 16 * CH + PER * W, B1 = B0 + PER;
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");
+}
+
+template <class C, bool ENC, int W>
+__device__ __forceinline__ void wave_run(const PsArgs &a, uint8_t *lds) {
+    constexpr int HI = ENC ? kN - (int)C::NR : kN;
+    constexpr uint32_t kTileBytes = 256u * 255u;
+    const pw_rsrc_t rsrc = pw_rsrc(a.base, a.span);
+    const uint32_t lbuf = __builtin_amdgcn_readfirstlane(lds_addr(lds));
+    const uint32_t ls0 = lbuf, ls1 = lbuf + (uint32_t)kSlot;
+    const pw_rsrc_t rout = pw_rsrc(reinterpret_cast<const uint8_t *>(a.result), ENC ? 0u : a.ncw * 4u);
+    const pw_rsrc_t rws = pw_rsrc(a.ws, ENC ? (uint32_t)(C::NR * a.ws_pitch) : (uint32_t)((a.ncw + 255) / 256 * kSynTile));
+    uint32_t off[kInstrW];
+    dma_offsets<W>(off);
+    uint32_t tile = blockIdx.x;
+    if (tile < a.ntiles) {
+        const uint32_t tb = tile * kTileBytes;
+        dma_run<W, 0, kInstrW>(off, ls0, tb, rsrc);
+        dma_run<W, 0, kInstrW>(off, ls1, tb + 128u, rsrc);
+    }
+    // stores this wave issued after the previous tile's chunk-1 DMAs (encode: fixed; decode: the
+    // results of wave 0 and, when the tile had a flagged codeword, the syndromes)
+    constexpr int NSYN = [] {
+        int n = 0;
+        for (int q = 0; q < C::NQ; ++q)
+            for (int j = 0; j < 4; ++j) n += C::SYN[W][q][j] >= 0;
+        return n;
+    }();
+    constexpr int NS0 = ENC ? NSYN : (W == 0 ? 4 : 0);
+    bool prev_flagged = false, first = true;
+    int pq_it = 0;
+    (void)pq_it;
+    PQ_RT(0);
+    for (; tile < a.ntiles; tile += gridDim.x, ++pq_it) {
+        PQ_STAMP(0);
+        const uint32_t next = tile + gridDim.x;
+        const bool has_next = next < a.ntiles;               // wave-uniform
+        const uint32_t tbn = next * kTileBytes;
+        uint32_t V[C::NI][8];                                // set by the wave's first block
+        // chunk 0 of this tile: every VMEM op but this wave's chunk-1 pieces and the stores after
+        // them has completed
+        if (first) wait_vm<kInstrW>();
+        else if (!ENC && prev_flagged) wait_vm<kInstrW + NS0 + NSYN>();
+        else wait_vm<kInstrW + NS0>();
+        pt::barrier();
+        PQ_STAMP(1);
+        asm volatile("s_setprio 1");
+        run<C, HI, 0, Blocks<ENC, W, 0>::B0, Blocks<ENC, W, 0>::B1, true>(V, ls0, [](auto) {});
+        asm volatile("s_setprio 0");
+        PQ_STAMP(2);
+        if (first) wait_vm<0>();                             // chunk 1 landed
+        else if (!ENC && prev_flagged) wait_vm<NS0 + NSYN>();
+        else wait_vm<NS0>();
+        first = false;
+        if (tile * kTileBytes + kTileBytes >= a.span && (a.span & 15u) != 0 && W == 0) {
+            // the last tile: a 16-byte piece that crosses the span's end came back all-zero; re-read
+            // its bytes inside the span one by one (out-of-range bytes read as zero) into the piece
+            const uint32_t pend = a.span & ~15u;             // the crossing piece's first byte
+            const uint32_t g = pend + pt::fresh();           // tile-relative offsets below
+            uint32_t v = 0;
+            if (pt::fresh() < 16u)
+                asm volatile("buffer_load_ubyte %0, %1, %2, 0 offen\n\ts_waitcnt vmcnt(0)"
+                             : "=&v"(v) : "v"(g), "s"(rsrc) : "memory");
+            const uint32_t t = g - tile * kTileBytes;         // the last row's chunk 1
+            const uint32_t r = (a.span - 1u - tile * kTileBytes) / 255u;
+            const uint32_t c1 = ((255u * r) & ~15u) + 128u; // its chunk-1 first piece
+            if (pt::fresh() < 16u && g < a.span && t >= c1 && t < c1 + (uint32_t)kPitch)
+                asm volatile("ds_write_b8 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                             :: "v"(ls1 + (uint32_t)kPitch * slot_pos(r) + (t - c1)), "v"(v) : "memory");
+        }
+        pt::barrier();                                       // chunk 1 visible; slot 0 consumed
+        PQ_STAMP(3);
+        asm volatile("s_setprio 1");
+        {
+            using BB = Blocks<ENC, W, 1>;
+            constexpr int NB = BB::B1 - BB::B0;
+            // the next tile's chunk 0 into slot 0, spread over this wave's chunk-1 blocks
+            run<C, HI, 1, BB::B0, BB::B1, false>(V, ls1, [&](auto bc) {
+                constexpr int i = decltype(bc)::value - BB::B0;
+                if (has_next) dma_run<W, (kInstrW * i + NB - 1) / NB, (kInstrW * (i + 1) + NB - 1) / NB>(off, ls0, tbn, rsrc);
+            });
+        }
+        asm volatile("s_setprio 0");
+        PQ_STAMP(4);
+        pt::barrier();                                       // slot 1 consumed
+        PQ_STAMP(5);
+        xpk::exchange<C, W>(V, ls1 + 16u * pt::fresh());
+        PQ_STAMP(6);
+        uint32_t T[C::NOWN][8];
+#pragma unroll
+        for (int i = 0; i < C::NOWN; ++i)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) T[i][t] = C::OWN[W][i] >= 0 ? V[C::OWN[W][i] < 0 ? 0 : C::OWN[W][i]][t] : 0u;
+        uint32_t Qs[C::NQ][8], nz = 0;
+        C::template epilogue<W>(T, [&](auto qc, uint32_t (&Qw)[8]) {
+            constexpr int qd = decltype(qc)::value;
+            constexpr uint32_t vm = (C::SYN[W][qd][0] >= 0 ? 0x01010101u : 0u) | (C::SYN[W][qd][1] >= 0 ? 0x02020202u : 0u) |
+                                    (C::SYN[W][qd][2] >= 0 ? 0x04040404u : 0u) | (C::SYN[W][qd][3] >= 0 ? 0x08080808u : 0u);
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                nz |= Qw[t] & vm;
+                Qs[qd][t] = Qw[t];
+            }
+        }, [&](auto pc) {
+            // the next tile's chunk 1 into slot 1 (released by the exchange), over the fold
+            constexpr int h = decltype(pc)::value;
+            if (has_next) {
+                if constexpr (h == 0) dma_run<W, 0, 2>(off, ls1, tbn + 128u, rsrc);
+                else dma_run<W, h + 1, h + 2>(off, ls1, tbn + 128u, rsrc);
+            }
+        });
+        if (has_next) dma_run<W, 4 * C::NQ + 1, kInstrW>(off, ls1, tbn + 128u, rsrc);   // (fewer hooks)
+        PQ_STAMP(7);
+        const uint32_t cw0 = tile * 256u + 4u * pt::fresh();  // byte k <-> codeword cw0 + k
+        if constexpr (ENC) {
+            static_for<0, C::NQ>([&](auto qc) {
+                constexpr int qd = decltype(qc)::value;
+                transpose8(Qs[qd]);                          // Qs[qd][jj] byte k: syndrome jj, codeword k
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj)
+                    if (C::SYN[W][qd][jj] >= 0)
+                        pt::store_dword(rws, (uint32_t)(C::SYN[W][qd][jj] * a.ws_pitch) + cw0, Qs[qd][jj]);
+            });
+        } else {
+            uint32_t fl = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (nz >> (8 * k) & 0xFF) fl |= 1u << k;
+            const uint32_t fa = lbuf + kFlags + 256u * W + 4u * pt::fresh();
+            asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" :: "v"(fa), "v"(fl) : "memory");
+            pt::barrier();
+            {
+                uint32_t f[4];
+                const uint32_t fb = lbuf + kFlags + 4u * pt::fresh();
+                asm volatile("ds_read_b32 %0, %4\n\t"
+                             "ds_read_b32 %1, %4 offset:256\n\t"
+                             "ds_read_b32 %2, %4 offset:512\n\t"
+                             "ds_read_b32 %3, %4 offset:768\n\t"
+                             "s_waitcnt lgkmcnt(0)"
+                             : "=&v"(f[0]), "=&v"(f[1]), "=&v"(f[2]), "=&v"(f[3]) : "v"(fb) : "memory");
+                fl = f[0] | f[1] | f[2] | f[3];
+            }
+            if constexpr (W == 0) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    pt::store_dword(rout, (cw0 + k) * 4u, (fl >> k & 1) ? (uint32_t)kSentinel : 0u);
+            }
+            prev_flagged = __ballot(fl != 0) != 0;           // wave-uniform (the same for all waves)
+            if (prev_flagged) {                              // flagged codewords: their syndromes
+                static_for<0, C::NQ>([&](auto qc) {
+                    constexpr int qd = decltype(qc)::value;
+                    transpose8(Qs[qd]);
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj)
+                        if (C::SYN[W][qd][jj] >= 0)
+                            pt::store_dword(rws, tile * (uint32_t)kSynTile + 256u * C::SYN[W][qd][jj] + 4u * pt::fresh(),
+                                            Qs[qd][jj]);
+                });
+            }
+        }
+    }
+    wait_vm<0>();                                            // no DMA may land after the exit
+    PQ_RT(1);
+}
+
+template <class C, bool ENC>
+__global__ void __attribute__((amdgpu_flat_work_group_size(kThreads, kThreads), amdgpu_waves_per_eu(2)))
+k_pq2(PsArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kLds];
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    switch (w) {
+    case 0: wave_run<C, ENC, 0>(a, lds); break;
+    case 1: wave_run<C, ENC, 1>(a, lds); break;
+    case 2: wave_run<C, ENC, 2>(a, lds); break;
+    default: wave_run<C, ENC, 3>(a, lds); break;
+    }
+}
+
+} // namespace pq2
 
 // ---- encode, stage 2: parity = V^-1 S on 32-codeword bit-sliced registers -------------------
 // Syndromes (encode workspace) -> parity rows.
@@ -1445,6 +1871,16 @@ void launch_tile(const ps::PsArgs &p, bool shard, unsigned grid, hipStream_t s) 
 #ifndef EZRS_NO_PQ
     if constexpr (!std::is_void<PQ>::value) {
         const bool lo0 = p.lo == 0;                          // full-length rows: no pad masks
+#ifdef EZRS_PQ2
+        // timing builds: plain batches of full-length packed rows from a 16-byte aligned base, each
+        // launch starting a tile of the syndrome layout, on the double-buffered kernel (r05e: C2
+        // 1381 vs 1450 GB/s -- its gathered DMA and the extra barriers cost more than the overlap
+        // gains; the early partial DMA of k_pq_lin is the default)
+        if (!shard && lo0 && p.stride == 255 && ((uintptr_t)p.base & 15) == 0 && (ENC || p.ws_pitch == 0)) {
+            hipLaunchKernelGGL((ps::pq2::k_pq2<PQ, ENC>), dim3(grid), dim3(ps::pq2::kThreads), 0, s, p);
+            return;
+        }
+#endif
         if (shard && lo0)
             hipLaunchKernelGGL((ps::pq::k_pq_lin<PQ, ENC, true, true>), dim3(grid), dim3(ps::pq::kThreads), 0, s, p);
         else if (shard)
