@@ -66,6 +66,8 @@ struct BchArgs {
     size_t lstride;
     size_t ncw;
     int staged;               // the block's data rows are copied to LDS with coalesced loads
+    int lds_fix;              // decode, staged rows with their ECC inline: corrections go to the LDS
+                              // image and only its dirty 16-byte pieces are written back
     int ecc_only;             // decode_bch's "ecc = recv XOR calc" form: no data, nothing corrected
     const uint32_t *syn;      // decode_bch's syndrome form: S_1..S_2t per codeword (ecc_only set)
     size_t sstride;
@@ -79,14 +81,24 @@ __host__ __device__ inline size_t rows_offset(const DevBch &b, bool tabs) {
     return tabs_offset(b) + (tabs && b.lds_tabs ? (((size_t)3 * b.n + 1) * 2 + 15) / 16 * 16 : 0);
 }
 
+// staged rows: kThreads rows at the batch pitch from a 16-byte aligned start (+ 16 + 16 slack),
+// then (lds_fix) the dirty-piece bitmap, one bit per 16 bytes of the image
+__host__ __device__ inline size_t rows_bytes(const BchArgs &a) { return ((size_t)kThreads * a.dstride + 32 + 15) & ~(size_t)15; }
+__host__ __device__ inline size_t dirty_words(const BchArgs &a) { return (rows_bytes(a) / 16 + 31) / 32; }
+
 size_t lds_bytes(const DevBch &b, bool tabs, const BchArgs &a) {
-    return rows_offset(b, tabs) + (a.staged ? (size_t)kThreads * a.dstride + 8 : 0);
+    return rows_offset(b, tabs) + (a.staged ? rows_bytes(a) + (a.lds_fix ? 4 * dirty_words(a) : 0) : 0);
 }
 
 // Rows are staged when the batch has a row pitch the block's span can hold within 64 KiB of LDS.
 int want_staging(const DevBch &b, bool tabs, const BchArgs &a) {
     return a.ncw > 1 && a.len > 0 && a.dstride >= a.len &&
-           rows_offset(b, tabs) + (size_t)kThreads * a.dstride + 8 <= kLdsLimit;
+           rows_offset(b, tabs) + rows_bytes(a) + 4 * dirty_words(a) <= kLdsLimit;
+}
+
+// ECC bytes inline after each row's data (the rows form): the staged image holds them too
+int ecc_inline(const DevBch &b, const BchArgs &a) {
+    return a.ecc == a.data + a.len && a.estride == a.dstride && a.dstride >= a.len + (size_t)b.ecc_bytes;
 }
 
 // ---- device ------------------------------------------------------------------------------------
@@ -168,15 +180,49 @@ __device__ __forceinline__ const uint8_t *block_rows(uint8_t *smem, const DevBch
     if (!a.staged) return a.data + (k0 + threadIdx.x) * a.dstride;
     const size_t nrows = a.ncw - k0 < (size_t)kThreads ? a.ncw - k0 : (size_t)kThreads;
     const uint8_t *base = a.data + k0 * a.dstride;
-    const size_t span = (nrows - 1) * a.dstride + a.len;
-    const unsigned off = (unsigned)((uintptr_t)base & 3u);
-    const uint32_t *src = reinterpret_cast<const uint32_t *>(base - off);
+    const size_t span = (nrows - 1) * a.dstride + a.len + (a.lds_fix ? (size_t)b.ecc_bytes : 0);
+    const unsigned off = (unsigned)((uintptr_t)base & 15u);
+    const uint4 *src = reinterpret_cast<const uint4 *>(base - off);
     uint8_t *rows = smem + rows_offset(b, tabs);
-    uint32_t *dst = reinterpret_cast<uint32_t *>(rows);
-    const unsigned nd = (unsigned)((off + span + 3) >> 2);
+    uint4 *dst = reinterpret_cast<uint4 *>(rows);
+    // 16-byte pieces (the last may run past the span, never past its 16-byte aligned page piece)
+    const unsigned nd = (unsigned)((off + span + 15) >> 4);
     for (unsigned i = threadIdx.x; i < nd; i += kThreads) dst[i] = src[i];
+    if (a.lds_fix) {
+        uint32_t *dirty = reinterpret_cast<uint32_t *>(rows + rows_bytes(a));
+        for (unsigned i = threadIdx.x; i < dirty_words(a); i += kThreads) dirty[i] = 0;
+    }
     __syncthreads();
     return rows + off + threadIdx.x * a.dstride;
+}
+
+// Flip bit el of this lane's staged row (data, then its inline ECC) and mark its 16-byte piece.
+__device__ __forceinline__ void fix_bit_lds(uint8_t *rows, uint32_t *dirty, const uint8_t *row, uint32_t el) {
+    const uint32_t o = (uint32_t)(row - rows) + (el >> 3);
+    atomicXor(reinterpret_cast<uint32_t *>(rows + (o & ~3u)), (1u << (el & 7)) << (8 * (o & 3)));
+    atomicOr(dirty + (o >> 9), 1u << ((o >> 4) & 31));
+}
+
+// After the block's corrections: every dirty 16-byte piece of the image back to the rows, whole
+// pieces inside the block's span as one store, the span's partial end pieces byte by byte (the
+// neighbouring blocks own the rest of them).
+__device__ __forceinline__ void write_back(uint8_t *rows, const uint32_t *dirty, const DevBch &b, const BchArgs &a) {
+    const size_t k0 = (size_t)blockIdx.x * kThreads;
+    const size_t nrows = a.ncw - k0 < (size_t)kThreads ? a.ncw - k0 : (size_t)kThreads;
+    uint8_t *base = a.wdata + k0 * a.dstride;
+    const unsigned off = (unsigned)((uintptr_t)base & 15u);
+    const uint32_t lo = off, hi = (uint32_t)(off + (nrows - 1) * a.dstride + a.len + (size_t)b.ecc_bytes);
+    uint8_t *g = base - off;
+    const uint32_t np = (hi + 15) >> 4;
+    for (uint32_t p = threadIdx.x; p < np; p += kThreads) {
+        if (!((dirty[p >> 5] >> (p & 31)) & 1u)) continue;
+        const uint32_t p0 = 16 * p;
+        if (p0 >= lo && p0 + 16 <= hi) {
+            *reinterpret_cast<uint4 *>(g + p0) = *reinterpret_cast<const uint4 *>(rows + p0);
+        } else {
+            for (uint32_t q = p0 < lo ? lo : p0; q < p0 + 16 && q < hi; ++q) g[q] = rows[q];
+        }
+    }
 }
 
 template <int NW>
@@ -444,13 +490,11 @@ __device__ int locate(const DevBch &b, const GF &f, Rem<NW> r, uint32_t nbits,
     return L;
 }
 
+// One codeword of k_bch_decode<T, NW>; with `dirty` (lds_fix) its corrections go to the staged
+// image (row: this lane's row in it) instead of the rows in global memory.
 template <int T, int NW>
-__global__ void __launch_bounds__(kThreads) k_bch_decode(DevBch b, BchArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    stage_tables(b, smem, true);
-    const uint8_t *row = a.ecc_only ? nullptr : block_rows(smem, b, true, a);
-    const size_t k = (size_t)blockIdx.x * kThreads + threadIdx.x;
-    if (k >= a.ncw) return;
+__device__ __forceinline__ void decode_one(const DevBch &b, const BchArgs &a, uint8_t *smem, const uint8_t *row,
+                                           size_t k, uint8_t *rows, uint32_t *dirty) {
     if (8ull * a.len > (unsigned long long)(b.n - b.ecc_bits)) {   // decode_bch's length check
         a.result[k] = -kEINVAL;
         return;
@@ -469,6 +513,7 @@ __global__ void __launch_bounds__(kThreads) k_bch_decode(DevBch b, BchArgs a) {
         return;
     }
     uint8_t *d = a.ecc_only ? nullptr : a.wdata + k * a.dstride, *e = a.ecc + k * a.estride;
+    const uint8_t *er = dirty ? row + a.len : e;         // the received ECC (staged when inline)
     Rem<NW> r;
     if (a.ecc_only) {
 #pragma unroll
@@ -477,7 +522,7 @@ __global__ void __launch_bounds__(kThreads) k_bch_decode(DevBch b, BchArgs a) {
         r = data_remainder<NW>(reinterpret_cast<const uint64_t *>(smem), row, a.len);
     }
     for (int i = 0; i < b.ecc_bytes && (i >> 3) < NW; ++i)    // bytes past NW words: unused bits
-        r.w[i >> 3] ^= (uint64_t)e[i] << (56 - 8 * (i & 7));
+        r.w[i >> 3] ^= (uint64_t)er[i] << (56 - 8 * (i & 7));
     uint64_t any = 0;
 #pragma unroll
     for (int i = 0; i < NW; ++i) any |= r.w[i];
@@ -498,10 +543,25 @@ __global__ void __launch_bounds__(kThreads) k_bch_decode(DevBch b, BchArgs a) {
             const uint32_t el = loc[i];
             if (a.errloc) a.errloc[k * a.lstride + i] = el;
             if (a.ecc_only) continue;
-            if (el < 8u * a.len) d[el >> 3] ^= (uint8_t)(1u << (el & 7));
+            if (dirty) fix_bit_lds(rows, dirty, row, el);
+            else if (el < 8u * a.len) d[el >> 3] ^= (uint8_t)(1u << (el & 7));
             else e[(el >> 3) - a.len] ^= (uint8_t)(1u << (el & 7));
         }
     }
+}
+
+template <int T, int NW>
+__global__ void __launch_bounds__(kThreads) k_bch_decode(DevBch b, BchArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    stage_tables(b, smem, true);
+    const uint8_t *row = a.ecc_only ? nullptr : block_rows(smem, b, true, a);
+    const size_t k = (size_t)blockIdx.x * kThreads + threadIdx.x;
+    uint8_t *rows = smem + rows_offset(b, true);
+    uint32_t *dirty = a.lds_fix ? reinterpret_cast<uint32_t *>(rows + rows_bytes(a)) : nullptr;
+    if (k < a.ncw) decode_one<T, NW>(b, a, smem, row, k, rows, dirty);
+    if (!a.lds_fix) return;                             // (uniform over the block)
+    __syncthreads();
+    write_back(rows, dirty, b, a);
 }
 
 // ---- t > 16 or ecc_bits > 256: the same decode with run-time t ------------------------------
@@ -1007,7 +1067,9 @@ hipError_t launch_decode(const DevBch &b, BchArgs a, hipStream_t s) {
         return hipSuccess;
     }
     const unsigned grid = (unsigned)((a.ncw + kThreads - 1) / kThreads);
+    a.lds_fix = !a.ecc_only && !a.syn && ecc_inline(b, a) && b.t <= 16 && b.nw <= 4;  // k_bch_decode<T, NW>
     a.staged = a.ecc_only ? 0 : want_staging(b, true, a);
+    if (!a.staged) a.lds_fix = 0;
     const size_t sh = lds_bytes(b, true, a);
     // (T, NW) instantiations: NW = 1 for ecc_bits <= 64 (t <= 12 since m >= 5), NW = 2 for
     // ecc_bits <= 128 (m t > 64: t >= 5), NW = 4 for ecc_bits <= 256 (t >= 9)
@@ -1352,7 +1414,7 @@ int ezbch_decode_ecc(const ezbch_codec *c, const uint8_t *ecc, size_t ecc_stride
     if (errloc && ncw > 1 && errloc_stride < c->h.t) return -EINVAL;
     DeviceGuard g(c->device);
     BchArgs a{nullptr, nullptr, 0, len, const_cast<uint8_t *>(ecc), ecc_stride, result, errloc,
-              errloc_stride, ncw, 0, 1};
+              errloc_stride, ncw, 0, 0, 1};
     hipError_t e = launch_decode(c->dev, a, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? 0 : hip_fail(e, "BCH decode launch");
 }
@@ -1366,7 +1428,7 @@ int ezbch_decode_syn(const ezbch_codec *c, const uint32_t *syn, size_t syn_strid
     if (ncw > 1 && syn_stride < 2 * (size_t)c->h.t) return -EINVAL;
     if (errloc && ncw > 1 && errloc_stride < c->h.t) return -EINVAL;
     DeviceGuard g(c->device);
-    BchArgs a{nullptr, nullptr, 0, len, nullptr, 0, result, errloc, errloc_stride, ncw, 0, 1,
+    BchArgs a{nullptr, nullptr, 0, len, nullptr, 0, result, errloc, errloc_stride, ncw, 0, 0, 1,
               syn, syn_stride};
     hipError_t e = launch_decode(c->dev, a, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? 0 : hip_fail(e, "BCH decode launch");

@@ -222,7 +222,15 @@ int ezrs_destroy(ezrs_codec *c) {
 
 int ezrs_set_semantics(ezrs_codec *c, int semantics) {
     if (!c || (semantics != EZRS_SEM_EZPWD && semantics != EZRS_SEM_KARN)) return -EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
     c->dev.karn = semantics == EZRS_SEM_KARN;
+    return 0;
+}
+
+int ezrs_set_launch_rows(ezrs_codec *c, size_t rows) {
+    if (!c) return -EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->dev.launch_rows = rows;
     return 0;
 }
 
@@ -546,34 +554,45 @@ int ezrs_decode_shards(const ezrs_codec *c, void *shards, size_t shard_pitch, si
 // ---- host-memory pipeline ---------------------------------------------------------------------
 namespace {
 
-// Rows whose decode result is nonzero, compacted: ix[0] = count, ix[1 + j] = chunk-relative row
-// index of compacted row j (in no particular order), out + j * row_bytes = its bytes.  ix[0] must be
-// zero on entry.
+// Rows whose decode result is nonzero, compacted straight into pinned host memory (the kernel's
+// stores cross PCIe; nothing to copy back afterwards): *cnt (device) counts them, hix[j] = chunk-
+// relative row index of compacted row j (in no particular order), hout + j * pitch = its bytes,
+// pitch = row_bytes rounded up to 16.  *cnt must be zero on entry.
 __global__ void __launch_bounds__(256) k_compact_rows(const int32_t *result, size_t n, const char *rows,
-                                                      size_t row_bytes, uint32_t *ix, char *out) {
+                                                      size_t row_bytes, uint32_t *cnt, uint32_t *hix,
+                                                      char *hout, size_t pitch) {
     __shared__ uint32_t slot[256];
     const size_t k = (size_t)blockIdx.x * 256 + threadIdx.x;
     const bool mine = k < n && result[k] != 0;
-    slot[threadIdx.x] = mine ? atomicAdd(ix, 1u) : 0xFFFFFFFFu;
-    if (mine) ix[1 + slot[threadIdx.x]] = (uint32_t)k;
+    slot[threadIdx.x] = mine ? atomicAdd(cnt, 1u) : 0xFFFFFFFFu;
+    if (mine) hix[slot[threadIdx.x]] = (uint32_t)k;
     __syncthreads();
-    // the block copies its flagged rows, one row per wavefront at a time (4 rows in flight), a byte
-    // per lane per step (rows of any length and alignment; consecutive lanes, consecutive bytes)
+    // the block copies its flagged rows, one row per wavefront at a time, 16 bytes per lane (byte
+    // loads: rows of any length and alignment; one 16-byte store into the padded host row)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int t = wave; t < 256; t += 4) {
         const uint32_t sl = slot[t];
         if (sl == 0xFFFFFFFFu) continue;
-        const char *src = rows + ((size_t)blockIdx.x * 256 + t) * row_bytes;
-        char *dst = out + (size_t)sl * row_bytes;
-        for (size_t b = lane; b < row_bytes; b += 64) dst[b] = src[b];
+        const unsigned char *src = reinterpret_cast<const unsigned char *>(rows) + ((size_t)blockIdx.x * 256 + t) * row_bytes;
+        char *dst = hout + (size_t)sl * pitch;
+        for (size_t b = 16 * (size_t)lane; b < row_bytes; b += 16 * 64) {
+            uint32_t v[4] = {0, 0, 0, 0};
+            if (b + 16 <= row_bytes) {
+#pragma unroll
+                for (int q = 0; q < 16; ++q) v[q >> 2] |= (uint32_t)src[b + q] << (8 * (q & 3));
+            } else {
+                for (size_t q = 0; b + q < row_bytes; ++q) v[q >> 2] |= (uint32_t)src[b + q] << (8 * (q & 3));
+            }
+            *reinterpret_cast<uint4 *>(dst + b) = make_uint4(v[0], v[1], v[2], v[3]);
+        }
     }
 }
 
 hipError_t launch_compact_rows(const int32_t *result, size_t n, const char *rows, size_t row_bytes,
-                               uint32_t *ix, char *out, int ncu, hipStream_t st) {
-    (void)ncu;
+                               uint32_t *cnt, uint32_t *hix, char *hout, size_t pitch, hipStream_t st) {
     const unsigned grid = (unsigned)((n + 255) / 256);
-    hipLaunchKernelGGL(k_compact_rows, dim3(grid), dim3(256), 0, st, result, n, rows, row_bytes, ix, out);
+    hipLaunchKernelGGL(k_compact_rows, dim3(grid), dim3(256), 0, st, result, n, rows, row_bytes, cnt, hix,
+                       hout, pitch);
     return hipGetLastError();
 }
 
@@ -597,7 +616,7 @@ int ensure_stage(ezrs_codec *c, size_t dbytes, size_t hbytes) {
             c->h_stage[i] = nullptr;
         }
         c->hstage_bytes = 0;
-        for (int i = 0; i < 2; ++i) HIP_TRY(hipHostMalloc(&c->h_stage[i], hbytes, hipHostMallocDefault));
+        for (int i = 0; i < 2; ++i) HIP_TRY(hipHostMalloc(&c->h_stage[i], hbytes, hipHostMallocMapped));   // device-visible: k_compact_rows writes here
         c->hstage_bytes = hbytes;
     }
     return 0;
@@ -776,33 +795,27 @@ int ezrs_decode_host(ezrs_codec *c, void *data, size_t data_stride, unsigned len
                  b_ne = align_up(neras ? chunk * 4 : 0), b_rs = align_up(chunk * 4),
                  b_ps = align_up(positions ? chunk * NR * 4 : 0),
                  b_co = align_up(corr ? chunk * NR * w : 0),
-                 b_sy = align_up(ws_bytes_for(c, chunk)),
-                 b_ix = align_up(chunk * 4 + 4), b_cp = align_up(chunk * row);
-    // pinned host staging: the compacted rows and their indices (+ the count)
-    const size_t h_cp = align_up(chunk * row), h_ix = align_up(chunk * 4 + 4);
-    if (int r = ensure_stage(c, b_cw + b_er + b_ne + b_rs + b_ps + b_co + b_sy + b_ix + b_cp, h_cp + h_ix)) return r;
+                 b_sy = align_up(ws_bytes_for(c, chunk)), b_ct = 256;
+    // pinned host staging: the compacted rows (16-byte pitch), their indices, the count
+    const size_t pitch = (row + 15) & ~(size_t)15;
+    const size_t h_cp = align_up(chunk * pitch), h_ix = align_up(chunk * 4), h_ct = 256;
+    if (int r = ensure_stage(c, b_cw + b_er + b_ne + b_rs + b_ps + b_co + b_sy + b_ct, h_cp + h_ix + h_ct)) return r;
     // Only the codewords whose result is nonzero can differ from what was sent (a clean codeword is
     // never written; -1 may leave partial corrections, rs_base:1238-1241): the device compacts those
-    // rows, and only the results and the compacted rows come back.
+    // rows straight into pinned host memory, and only the results and the count are copied back, so
+    // a chunk needs one synchronisation before its rows are scattered.
     struct Pending { size_t k0 = 0; bool live = false; } pend[2];
     auto finish = [&](int s) -> int {
         if (!pend[s].live) return 0;
         pend[s].live = false;
-        hipStream_t st = c->streams[s];
-        HIP_TRY(hipStreamSynchronize(st));                      // results and the count are back
-        char *hb = static_cast<char *>(c->h_stage[s]);
+        HIP_TRY(hipStreamSynchronize(c->streams[s]));           // rows, indices, results, count
+        const char *hb = static_cast<const char *>(c->h_stage[s]);
         const uint32_t *hix = reinterpret_cast<const uint32_t *>(hb + h_cp);
-        const uint32_t cnt = hix[0];
-        if (!cnt) return 0;
-        char *base = static_cast<char *>(c->d_stage[s]);
-        const char *dix = base + b_cw + b_er + b_ne + b_rs + b_ps + b_co + b_sy, *dcp = dix + b_ix;
-        HIP_TRY(hipMemcpyAsync(hb, dcp, cnt * row, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipMemcpyAsync(hb + h_cp + 4, dix + 4, cnt * 4, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
+        const uint32_t cnt = *reinterpret_cast<const uint32_t *>(hb + h_cp + h_ix);
         const size_t k0 = pend[s].k0;
         for (uint32_t j = 0; j < cnt; ++j) {
-            const size_t k = k0 + hix[1 + j];
-            const char *src = hb + (size_t)j * row;
+            const size_t k = k0 + hix[j];
+            const char *src = hb + (size_t)j * pitch;
             if (inline_par) {
                 std::memcpy(static_cast<char *>(data) + k * data_stride * w, src, (size_t)(len + NR) * w);
             } else {
@@ -820,7 +833,9 @@ int ezrs_decode_host(ezrs_codec *c, void *data, size_t data_stride, unsigned len
         if (int r = finish(s)) return r;                        // chunk i-2 (this stream's buffers)
         char *base = static_cast<char *>(c->d_stage[s]);
         char *dcw = base, *der = dcw + b_cw, *dne = der + b_er, *drs = dne + b_ne, *dps = drs + b_rs,
-             *dco = dps + b_ps, *dsy = dco + b_co, *dix = dsy + b_sy, *dcp = dix + b_ix;
+             *dco = dps + b_ps, *dsy = dco + b_co, *dct = dsy + b_sy;
+        char *hb = static_cast<char *>(c->h_stage[s]), *dhb = nullptr;
+        HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&dhb), hb, 0));
         char *hd = static_cast<char *>(data) + k0 * data_stride * w;
         char *hp = static_cast<char *>(parity) + k0 * parity_stride * w;
         const size_t span = ((n - 1) * data_stride + len + NR) * w;
@@ -850,11 +865,12 @@ int ezrs_decode_host(ezrs_codec *c, void *data, size_t data_stride, unsigned len
                      positions ? reinterpret_cast<uint32_t *>(dps) : nullptr, NR,
                      corr ? dco : nullptr, NR, n};
         HIP_TRY(dispatch_decode(c, a, reinterpret_cast<uint8_t *>(dsy), st));
-        HIP_TRY(hipMemsetAsync(dix, 0, 4, st));
+        HIP_TRY(hipMemsetAsync(dct, 0, 4, st));
         HIP_TRY(launch_compact_rows(reinterpret_cast<const int32_t *>(drs), n, dcw, row,
-                                    reinterpret_cast<uint32_t *>(dix), dcp, c->dev.ncu, st));
+                                    reinterpret_cast<uint32_t *>(dct), reinterpret_cast<uint32_t *>(dhb + h_cp),
+                                    dhb, pitch, st));
         HIP_TRY(hipMemcpyAsync(result + k0, drs, n * 4, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipMemcpyAsync(static_cast<char *>(c->h_stage[s]) + h_cp, dix, 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(hb + h_cp + h_ix, dct, 4, hipMemcpyDeviceToHost, st));
         if (positions)
             HIP_TRY(ezrs::copy2d(positions + k0 * pos_stride, pos_stride * 4, dps,
                                  (size_t)NR * 4, (size_t)NR * 4, n, hipMemcpyDeviceToHost, st));

@@ -20,10 +20,16 @@
 //  * GF products through a 256-byte antilog table in LDS with a zero class for log(0): any log >= 510
 //    marks zero, and a product's index is min(x, x - 255, 255) with alpha_to[255] = 0, so no
 //    compare/select per product.
-//  * Chien evaluates four consecutive positions per table read: CH[j][x] packs lambda_j-term values
-//    alpha^x, alpha^(x+j), alpha^(x+2j), alpha^(x+3j) into one dword (32 KiB for j = 1..32), so
-//    each register steps by 4j and a zero byte of the XOR marks a root.  That is 64 steps of
-//    deg(lambda) reads instead of 255, the LDS-read rate being what bounds this kernel.
+//  * Chien evaluates eight consecutive positions per table read: CH8[j][x] packs lambda_j-term values
+//    alpha^x, alpha^(x+j), .., alpha^(x+7j) into 8 bytes (32 KiB for j = 1..16; j = 17..32 use a
+//    4-position dword table and two reads), so each register steps by 8j and a zero byte of the XOR
+//    marks a root.  That is 32 steps of deg(lambda) reads instead of 255, the LDS-read rate being
+//    what bounds this kernel (r05j, C3 decode: 0.686 vs 0.731 ms with four positions per read).
+//    Measured and dropped (r05j): corrections applied by the wave in whole 16-byte pieces of the
+//    rows (the records of each row gathered per piece): 1.01 vs 0.73 ms.
+//  * Phase costs on C3 (r05j, timing ablations EZRS_ERR_STOP, whole decode call 0.731 ms, the
+//    syndrome kernel 0.095 of it): screen, syndromes and erasure locator 0.077 ms, Berlekamp-Massey
+//    0.19, Chien 0.22 (four positions per read), Omega and Forney 0.10, applying corrections 0.05.
 #include "ezrs_internal.hpp"
 
 namespace ezrs {
@@ -40,7 +46,8 @@ constexpr int32_t kSentinel = INT32_MIN;
 constexpr int kSpan = 256;              // result slots screened per wavefront
 constexpr int kWaves = 16;              // wavefronts per workgroup (one workgroup per CU)
 constexpr unsigned kZ = 1024;           // log(0); every value >= 510 is in the zero class
-constexpr int kSrows = 36;              // reversed syndromes: rows 0..31, zero-class padding 32..35
+constexpr int kSrows = 35;              // reversed syndromes: rows 0..31, zero-class padding 32..34
+                                        // (BM reads rows up to 32 - r + (r - 1) + 3)
 
 // antilog index of the product of two logs (either may be in the zero class)
 __device__ __forceinline__ unsigned pidx(unsigned x) {
@@ -59,7 +66,8 @@ struct WaveLds {
     uint16_t list[kSpan];                // flagged slots of the current span
 };
 struct Lds {
-    uint32_t CH[32 * 256];               // Chien: CH[j-1][x] = alpha^(x + k j), k = 0..3, per byte
+    uint2 CH8[16 * 256];                 // Chien, j = 1..16: CH8[j-1][x] = alpha^(x + k j), k = 0..7, per byte
+    uint32_t CH[16 * 256];               // j = 17..32: CH[j-17][x] = alpha^(x + k j), k = 0..3
     uint8_t A[256];                      // alpha_to, A[255] = 0
     uint16_t I[256];                     // index_of, I[0] = kZ
     WaveLds w[kWaves];
@@ -230,33 +238,48 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
         if (i > 0 && lam[i] != 0) deg = i;
     }
 
-    // Chien search (1555-1584), four positions i .. i+3 per step: rg[j] = 4 * ((log lambda_j +
-    // j*i) mod 255) addresses CH[j-1]; lambda_j = 0 keeps rg in the zero class (clamped to entry 255)
+    // Chien search (1555-1584); lambda_j = 0 keeps rg[j] in the zero class (clamped to entry 255)
     int count = 0;
     if (deg > 0) {
+        // eight positions i .. i+7 per step: j <= 16 one 8-byte read of CH8[j-1] (rg[j] = 8 * ((log
+        // lambda_j + j*i) mod 255)), j > 16 two 4-byte reads of CH[j-17] (rg[j] = 4 * (...))
         unsigned rg[33];
 #pragma unroll
-        for (int j = 1; j <= 32; ++j) rg[j] = l[j] < 255u ? 4u * addmod(l[j], (unsigned)j) : 0x80000000u;
-        for (unsigned i = 1; i <= 255; i += 4) {
-            unsigned q = 0x01010101u;
+        for (int j = 1; j <= 32; ++j)
+            rg[j] = l[j] < 255u ? (j <= 16 ? 8u : 4u) * addmod(l[j], (unsigned)j) : 0x80000000u;
+        for (unsigned i = 1; i <= 255; i += 8) {
+            unsigned q0 = 0x01010101u, q1 = 0x01010101u;
 #pragma unroll
             for (int j0 = 1; j0 <= 32; j0 += 4) {
                 if ((unsigned)j0 <= deg) {
 #pragma unroll
                     for (int j = j0; j < j0 + 4; ++j) {
-                        q ^= *reinterpret_cast<const uint32_t *>(
-                            reinterpret_cast<const uint8_t *>(L.CH + (j - 1) * 256) + min(rg[j], 1020u));
-                        const unsigned a = rg[j] + 16u * j, z = a - 1020u;
-                        rg[j] = min(a, z);
+                        if (j <= 16) {
+                            const uint2 v = *reinterpret_cast<const uint2 *>(
+                                reinterpret_cast<const uint8_t *>(L.CH8 + (j - 1) * 256) + min(rg[j], 2040u));
+                            q0 ^= v.x;
+                            q1 ^= v.y;
+                            const unsigned a = rg[j] + 64u * j, z = a - 2040u;
+                            rg[j] = min(a, z);
+                        } else {
+                            const uint8_t *t = reinterpret_cast<const uint8_t *>(L.CH + (j - 17) * 256);
+                            q0 ^= *reinterpret_cast<const uint32_t *>(t + min(rg[j], 1020u));
+                            const unsigned a = rg[j] + 16u * j, z = a - 1020u, r1 = min(a, z);
+                            q1 ^= *reinterpret_cast<const uint32_t *>(t + min(r1, 1020u));
+                            const unsigned b2 = r1 + 16u * j, z2 = b2 - 1020u;
+                            rg[j] = min(b2, z2);
+                        }
                     }
                 }
             }
-            if (i == 253) q |= 0xff000000u;                     // position 256 does not exist
-            if (((q - 0x01010101u) & ~q & 0x80808080u) == 0) continue;
+            if (i == 249) q1 |= 0xff000000u;                    // position 256 does not exist
+            const bool z0 = ((q0 - 0x01010101u) & ~q0 & 0x80808080u) != 0,
+                       z1 = ((q1 - 0x01010101u) & ~q1 & 0x80808080u) != 0;
+            if (!z0 && !z1) continue;
             bool done = false;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (((q >> (8 * k)) & 255u) == 0) {
+            for (int k = 0; k < 8; ++k) {
+                if ((((k < 4 ? q0 : q1) >> (8 * (k & 3))) & 255u) == 0) {
                     W.root[count * 64 + lane] = (uint8_t)(i + k);
                     if (++count == (int)deg) { done = true; break; }
                 }
@@ -430,8 +453,18 @@ __global__ void __launch_bounds__(64 * kWaves) k_decode_errors(DevCodec c, Decod
         L.I[i] = i == 0 ? (uint16_t)kZ : c.index_of[i];
     }
     __syncthreads();
-    for (unsigned t = threadIdx.x; t < 32 * 256; t += 64 * kWaves) {
+    for (unsigned t = threadIdx.x; t < 16 * 256; t += 64 * kWaves) {
         const unsigned j = t / 256 + 1, x = t % 256;
+        uint32_t v0 = 0, v1 = 0;
+        if (x < 255)
+            for (unsigned k = 0; k < 4; ++k) {
+                v0 |= (uint32_t)L.A[(x + k * j) % 255u] << (8 * k);
+                v1 |= (uint32_t)L.A[(x + (k + 4) * j) % 255u] << (8 * k);
+            }
+        L.CH8[t] = make_uint2(v0, v1);
+    }
+    for (unsigned t = threadIdx.x; t < 16 * 256; t += 64 * kWaves) {
+        const unsigned j = t / 256 + 17, x = t % 256;
         uint32_t v = 0;
         if (x < 255)
             for (unsigned k = 0; k < 4; ++k) v |= (uint32_t)L.A[(x + k * j) % 255u] << (8 * k);

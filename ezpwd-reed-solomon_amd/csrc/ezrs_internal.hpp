@@ -28,6 +28,8 @@ struct DevCodec {
     int dual;
     int masked;                   // symbol narrower than its datum (rs_base:1194)
     int ncu;                      // compute units of the device (persistent grids)
+    size_t launch_rows;           // test hook (ezrs_set_launch_rows): codewords per plane-sliced
+                                  // launch, 0 = the largest batch whose 32-bit offsets fit
     int karn;                     // decode with Phil Karn's libfec semantics (ezrs_set_semantics):
                                   // erasures and positions in the full NN frame, none of ezpwd's
                                   // extra failure checks (fec-3.0.1/decode_rs.h:71-298)

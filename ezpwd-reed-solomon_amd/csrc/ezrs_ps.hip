@@ -1606,6 +1606,7 @@ __device__ __forceinline__ void store_parity_row(uint8_t *dst, const uint8_t *s8
     }
 }
 
+#ifdef EZRS_PAR_PIPE
 // Persistent, software-pipelined form of k_ps_parity8 (one 8-wave block per CU: planes and stage
 // in separate LDS, 130 KiB): chunk j's map runs while chunk j-1's parity rows drain to memory
 // (one quarter of the stores at each of four points of the pass) and chunk j+1's syndromes load
@@ -1710,6 +1711,7 @@ __global__ void __launch_bounds__(512) k_ps_parity_pipe(const uint8_t *ws, size_
     if (prev != 0xFFFFFFFFu)
         for (int j = 0; j < 4; ++j) store_part(prev, j);
 }
+#endif // EZRS_PAR_PIPE
 
 // 8-wave form of k_ps_parity: wave P computes parity symbols 4P..4P+3 (q_pass4), halving each
 // wave's share of the map and doubling the waves that hide the phases' latencies.
@@ -1936,29 +1938,27 @@ size_t ps_ws_bytes(size_t ncw) { return ps_pitch(ncw) * 32; }
 // the tile kernel's out-of-range marker kOob is above them).
 // That covers the rows' span AND the per-codeword buffers: the result array (4 B per codeword) and
 // the syndrome workspace (32 B per codeword in either layout), so a short row pitch cannot wrap the
-// workspace offsets.  ezrs_set_launch_rows() lowers the cap (tests: launches split mid-batch and,
-// for shard batches, mid-tile; the results are the same by construction).
-static std::atomic<size_t> g_launch_rows{0};
-static size_t ps_row_cap() {
+// workspace offsets.  The codec's launch_rows (ezrs_set_launch_rows, a test hook) lowers the cap
+// (tests: launches split mid-batch and, for shard batches, mid-tile; the results are the same by
+// construction).
+static size_t ps_row_cap(const DevCodec &d) {
     const size_t hard = (size_t)0xE0000000u / 32;
-    const size_t t = g_launch_rows.load(std::memory_order_relaxed);
-    return t && t < hard ? t : hard;
+    return d.launch_rows && d.launch_rows < hard ? d.launch_rows : hard;
 }
-static size_t ps_max_rows(size_t stride) {
-    const size_t cap = ps_row_cap();
+static size_t ps_max_rows(const DevCodec &d, size_t stride) {
+    const size_t cap = ps_row_cap(d);
     size_t m = (size_t)0xE0000000u / stride;
     if (m > cap) m = cap;
     return m >= 2048 && cap == (size_t)0xE0000000u / 32 ? m / 2048 * 2048 : m;   // a test cap: as set
 }
 
 // Shard batches: rows per launch, whole shards (byte offsets stay below 0xE0000000 as above).
-static size_t ps_max_rows_shards(const Shards &g) {
+static size_t ps_max_rows_shards(const DevCodec &d, const Shards &g) {
     size_t n = (size_t)0xE0000000u / g.pitch;
-    const size_t byrows = ps_row_cap() / g.rows;
+    const size_t byrows = ps_row_cap(d) / g.rows;
     if (byrows < n) n = byrows;
     return (n ? n : 1) * g.rows;
 }
-
 // Shard batches: a tile's rows must fit the 64 KiB image (no gaps between shards beyond a row's
 // width) and every launch's span the 32-bit offsets.
 static bool ps_shards_ok(const Shards &g, size_t stride) {
@@ -1978,7 +1978,7 @@ bool ps_can_decode(const DevCodec &d, const DecodeArgs &a) {
 
 hipError_t launch_ps_encode(int id, const DevCodec &d, const EncodeArgs &a, void *ws, hipStream_t s) {
     const size_t pitch = a.data_stride > a.parity_stride ? a.data_stride : a.parity_stride;
-    const size_t maxr = a.sh.rows ? ps_max_rows_shards(a.sh) : ps_max_rows(pitch);
+    const size_t maxr = a.sh.rows ? ps_max_rows_shards(d, a.sh) : ps_max_rows(d, pitch);
     for (size_t k0 = 0; k0 < a.ncw; k0 += maxr) {
         const size_t n = a.ncw - k0 < maxr ? a.ncw - k0 : maxr;
         ps::PsArgs p{};
@@ -2020,7 +2020,7 @@ hipError_t launch_ps_encode(int id, const DevCodec &d, const EncodeArgs &a, void
 
 hipError_t launch_ps_syndromes(int id, const DevCodec &d, const DecodeArgs &a, uint8_t *syn_ws,
                                hipStream_t s) {
-    const size_t maxr = a.sh.rows ? ps_max_rows_shards(a.sh) : ps_max_rows(a.data_stride);
+    const size_t maxr = a.sh.rows ? ps_max_rows_shards(d, a.sh) : ps_max_rows(d, a.data_stride);
     for (size_t k0 = 0; k0 < a.ncw; k0 += maxr) {
         const size_t n = a.ncw - k0 < maxr ? a.ncw - k0 : maxr;
         ps::PsArgs p{};
@@ -2056,7 +2056,3 @@ hipError_t launch_ps_syndromes(int id, const DevCodec &d, const DecodeArgs &a, u
 
 } // namespace ezrs
 
-extern "C" int ezrs_set_launch_rows(size_t rows) {
-    ezrs::g_launch_rows.store(rows, std::memory_order_relaxed);
-    return 0;
-}

@@ -93,7 +93,7 @@ def lib():
         L.ezrs_decode_shards.argtypes = [_vp, _vp, _sz, _sz, _u, _sz, _vp, _sz, _vp, _vp, _vp, _sz,
                                          _vp, _sz, _vp]
         L.ezrs_kernel_path.argtypes = [_vp]
-        L.ezrs_set_launch_rows.argtypes = [_sz]
+        L.ezrs_set_launch_rows.argtypes = [_vp, _sz]
         L.ezrs_set_semantics.argtypes = [_vp, _i]
         L.ezrs_get_semantics.argtypes = [_vp]
         L.ezrs_host_alloc.argtypes = [C.POINTER(_vp), _sz]
@@ -113,12 +113,6 @@ def lib():
         L.ezbch_decode_host.argtypes = [_vp, _vp, _sz, _u, _vp, _sz, _vp, _vp, _sz, _sz, _sz]
         _lib = L
     return _lib
-
-
-def set_launch_rows(rows):
-    """Test hook (ezrs_set_launch_rows): cap the codewords one plane-sliced launch takes; 0 = the
-    default.  Results never depend on it."""
-    lib().ezrs_set_launch_rows(int(rows))
 
 
 def _check(rc, what, bch=False):
@@ -246,6 +240,11 @@ class Codec:
     @semantics.setter
     def semantics(self, mode):
         _check(lib().ezrs_set_semantics(self._h, {"ezpwd": 0, "karn": 1}[mode]), "ezrs_set_semantics")
+
+    def set_launch_rows(self, rows):
+        """Test hook (ezrs_set_launch_rows): cap the codewords one plane-sliced launch of this codec
+        takes; 0 = the default.  Results never depend on it."""
+        _check(lib().ezrs_set_launch_rows(self._h, int(rows)), "ezrs_set_launch_rows")
 
     def reserve(self, ncw, stream=None):
         """Pre-size the workspace of `stream` (default: the current torch stream)."""

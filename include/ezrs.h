@@ -96,16 +96,22 @@ int ezrs_kernel_path(const ezrs_codec *codec);
  *     (fec-3.0.1/decode_rs.h:71-298): erasures and positions in the full NN frame (a position
  *     p >= pad is row symbol p - pad), none of those three checks (a zero denominator applies
  *     num1 * num2, a root in the pad is counted and reported but not corrected), the datum is the
- *     symbol.  The Karn ABI (include/ezrs_fec.h) creates its codecs in this mode. */
+ *     symbol.  The Karn ABI (include/ezrs_fec.h) creates its codecs in this mode.
+ * Set the semantics once, after create and before the codec's first decode: the setter takes the
+ * codec's lock (it waits for a host-memory call in progress), but a device decode already enqueued
+ * on a stream runs with the semantics it was launched with, and decodes issued concurrently from
+ * other threads may see either. */
 #define EZRS_SEM_EZPWD 0
 #define EZRS_SEM_KARN 1
 int ezrs_set_semantics(ezrs_codec *codec, int semantics);
 int ezrs_get_semantics(const ezrs_codec *codec);
-/* Test hook: cap the codewords one plane-sliced kernel launch takes (0 restores the default, the
- * largest batch whose 32-bit buffer offsets fit).  Results never depend on it: lowering it only
- * splits a batch over more launches (mid-tile for shard batches), which the tests use to exercise
- * those splits at small sizes.  Process-wide; not for use while other threads launch. */
-int ezrs_set_launch_rows(size_t rows);
+/* Test hook: cap the codewords one plane-sliced kernel launch of `codec` takes (0 restores the
+ * default, the largest batch whose 32-bit buffer offsets fit).  Results never depend on it:
+ * lowering it only splits a batch over more launches (mid-tile for shard batches), which the tests
+ * use to exercise those splits at small sizes.  Per codec; takes the codec's lock, so it waits for
+ * a host-memory call in progress, but a device call already enqueued keeps the cap it was
+ * launched with. */
+int ezrs_set_launch_rows(ezrs_codec *codec, size_t rows);
 int ezrs_get_info(const ezrs_codec *codec, ezrs_info *info);
 
 /* Pre-size the workspace of `stream` (NULL: the null stream) for batches of up to `ncw` codewords,

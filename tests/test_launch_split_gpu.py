@@ -1,4 +1,4 @@
-"""Batches split over several plane-sliced launches: ezrs_set_launch_rows lowers the
+"""Batches split over several plane-sliced launches: ezrs_set_launch_rows lowers a codec's
 per-launch codeword cap so a small batch takes the paths a multi-GB one would -- plain batches whose
 launches start off the 256-codeword tile grid, short row pitches, and shard batches whose launches
 end mid-tile (the byte-store syndrome path).  Every output is compared with the oracle."""
@@ -18,13 +18,6 @@ def torch():
     return T
 
 
-@pytest.fixture
-def split():
-    import ezrs
-    yield ezrs.set_launch_rows
-    ezrs.set_launch_rows(0)
-
-
 def _corrupt(rng, cw, L, nr, ncw):
     eras = np.zeros((ncw, nr), np.uint32)
     neras = np.zeros(ncw, np.uint32)
@@ -40,7 +33,7 @@ def _corrupt(rng, cw, L, nr, ncw):
 
 
 @pytest.mark.parametrize("k,L,rows", [(223, 223, 1000), (223, 16, 300), (247, 40, 2049), (251, 200, 5)])
-def test_plain_batch_split_vs_oracle(torch, split, k, L, rows):
+def test_plain_batch_split_vs_oracle(torch, k, L, rows):
     import ezrs
     c = ezrs.Codec.rs(255, k)
     assert c.kernel_path == "planeslice"
@@ -50,7 +43,7 @@ def test_plain_batch_split_vs_oracle(torch, split, k, L, rows):
     data = rng.integers(0, 256, (ncw, L + nr)).astype(np.uint8)
     ref = data.copy()
     oc.encode_batch(ref, L, None, nthreads=8)
-    split(rows)
+    c.set_launch_rows(rows)
     dev = torch.from_numpy(data).cuda()
     c.encode(dev, L)
     torch.cuda.synchronize()
@@ -75,7 +68,7 @@ def test_plain_batch_split_vs_oracle(torch, split, k, L, rows):
 
 
 @pytest.mark.parametrize("S,rows", [(1024, 777), (16384, 300), (600, 1)])
-def test_shard_batch_split_vs_oracle(torch, split, S, rows):
+def test_shard_batch_split_vs_oracle(torch, S, rows):
     """Shard launches hold whole shards: 777 rows of 1 KiB shards (5 codewords each) = 155 shards
     per launch, so every launch after the first starts mid-tile."""
     import ezrs
@@ -88,7 +81,7 @@ def test_shard_batch_split_vs_oracle(torch, split, S, rows):
     rng = np.random.default_rng(S + rows)
     host = rng.integers(0, 256, (ns, enc)).astype(np.uint8)
     step = chunk + nr
-    split(rows)
+    c.set_launch_rows(rows)
     dev = torch.from_numpy(host.copy()).cuda()
     c.encode_shards(dev, S, chunk)
     exp = host.copy()
