@@ -67,7 +67,7 @@ struct BchArgs {
     size_t ncw;
     int staged;               // the block's data rows are copied to LDS with coalesced loads
     int lds_fix;              // decode, staged rows with their ECC inline: corrections go to the LDS
-                              // image and only its dirty 16-byte pieces are written back
+                              // image and only the 16-byte pieces holding them are written back
     int ecc_only;             // decode_bch's "ecc = recv XOR calc" form: no data, nothing corrected
     const uint32_t *syn;      // decode_bch's syndrome form: S_1..S_2t per codeword (ecc_only set)
     size_t sstride;
@@ -81,19 +81,18 @@ __host__ __device__ inline size_t rows_offset(const DevBch &b, bool tabs) {
     return tabs_offset(b) + (tabs && b.lds_tabs ? (((size_t)3 * b.n + 1) * 2 + 15) / 16 * 16 : 0);
 }
 
-// staged rows: kThreads rows at the batch pitch from a 16-byte aligned start (+ 16 + 16 slack),
-// then (lds_fix) the dirty-piece bitmap, one bit per 16 bytes of the image
-__host__ __device__ inline size_t rows_bytes(const BchArgs &a) { return ((size_t)kThreads * a.dstride + 32 + 15) & ~(size_t)15; }
-__host__ __device__ inline size_t dirty_words(const BchArgs &a) { return (rows_bytes(a) / 16 + 31) / 32; }
+// staged rows: kThreads rows at the batch pitch from a dword-aligned start (+ 3 + 3 slack; C5's
+// 256 rows of 127 bytes then fit four blocks per CU)
+__host__ __device__ inline size_t rows_bytes(const BchArgs &a) { return (size_t)kThreads * a.dstride + 8; }
 
 size_t lds_bytes(const DevBch &b, bool tabs, const BchArgs &a) {
-    return rows_offset(b, tabs) + (a.staged ? rows_bytes(a) + (a.lds_fix ? 4 * dirty_words(a) : 0) : 0);
+    return rows_offset(b, tabs) + (a.staged ? rows_bytes(a) : 0);
 }
 
 // Rows are staged when the batch has a row pitch the block's span can hold within 64 KiB of LDS.
 int want_staging(const DevBch &b, bool tabs, const BchArgs &a) {
     return a.ncw > 1 && a.len > 0 && a.dstride >= a.len &&
-           rows_offset(b, tabs) + rows_bytes(a) + 4 * dirty_words(a) <= kLdsLimit;
+           rows_offset(b, tabs) + rows_bytes(a) <= kLdsLimit;
 }
 
 // ECC bytes inline after each row's data (the rows form): the staged image holds them too
@@ -181,46 +180,53 @@ __device__ __forceinline__ const uint8_t *block_rows(uint8_t *smem, const DevBch
     const size_t nrows = a.ncw - k0 < (size_t)kThreads ? a.ncw - k0 : (size_t)kThreads;
     const uint8_t *base = a.data + k0 * a.dstride;
     const size_t span = (nrows - 1) * a.dstride + a.len + (a.lds_fix ? (size_t)b.ecc_bytes : 0);
-    const unsigned off = (unsigned)((uintptr_t)base & 15u);
-    const uint4 *src = reinterpret_cast<const uint4 *>(base - off);
+    const unsigned off = (unsigned)((uintptr_t)base & 3u);
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(base - off);
     uint8_t *rows = smem + rows_offset(b, tabs);
-    uint4 *dst = reinterpret_cast<uint4 *>(rows);
-    // 16-byte pieces (the last may run past the span, never past its 16-byte aligned page piece)
-    const unsigned nd = (unsigned)((off + span + 15) >> 4);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(rows);
+    const unsigned nd = (unsigned)((off + span + 3) >> 2);
     for (unsigned i = threadIdx.x; i < nd; i += kThreads) dst[i] = src[i];
-    if (a.lds_fix) {
-        uint32_t *dirty = reinterpret_cast<uint32_t *>(rows + rows_bytes(a));
-        for (unsigned i = threadIdx.x; i < dirty_words(a); i += kThreads) dirty[i] = 0;
-    }
     __syncthreads();
     return rows + off + threadIdx.x * a.dstride;
 }
 
-// Flip bit el of this lane's staged row (data, then its inline ECC) and mark its 16-byte piece.
-__device__ __forceinline__ void fix_bit_lds(uint8_t *rows, uint32_t *dirty, const uint8_t *row, uint32_t el) {
+// Flip bit el of this lane's staged row (data, then its inline ECC).
+__device__ __forceinline__ void fix_bit_lds(uint8_t *rows, const uint8_t *row, uint32_t el) {
     const uint32_t o = (uint32_t)(row - rows) + (el >> 3);
     atomicXor(reinterpret_cast<uint32_t *>(rows + (o & ~3u)), (1u << (el & 7)) << (8 * (o & 3)));
-    atomicOr(dirty + (o >> 9), 1u << ((o >> 4) & 31));
 }
 
-// After the block's corrections: every dirty 16-byte piece of the image back to the rows, whole
-// pieces inside the block's span as one store, the span's partial end pieces byte by byte (the
-// neighbouring blocks own the rest of them).
-__device__ __forceinline__ void write_back(uint8_t *rows, const uint32_t *dirty, const DevBch &b, const BchArgs &a) {
+// Once every lane of the wave has flipped its bits in the image: each lane writes back the 16-byte
+// pieces (on the global 16-byte grid) that hold its corrected bits, from the image -- a piece wholly
+// inside the bytes of the wave's 64 rows as one store (a piece shared by two rows of the wave may
+// be written by both lanes, with the same bytes), a piece reaching past them byte by byte over the
+// wave's own bytes only (the neighbouring waves and blocks write the rest).
+template <int T>
+__device__ __forceinline__ void write_pieces(const uint8_t *rows, const uint8_t *row, const uint32_t (&loc)[T], int cnt,
+                                             const DevBch &b, const BchArgs &a) {
     const size_t k0 = (size_t)blockIdx.x * kThreads;
     const size_t nrows = a.ncw - k0 < (size_t)kThreads ? a.ncw - k0 : (size_t)kThreads;
+    const unsigned w = threadIdx.x >> 6;
+    const size_t wend = 64u * w + 64u < nrows ? 64u * w + 64u : nrows;     // the wave's rows [64 w, wend)
     uint8_t *base = a.wdata + k0 * a.dstride;
-    const unsigned off = (unsigned)((uintptr_t)base & 15u);
-    const uint32_t lo = off, hi = (uint32_t)(off + (nrows - 1) * a.dstride + a.len + (size_t)b.ecc_bytes);
-    uint8_t *g = base - off;
-    const uint32_t np = (hi + 15) >> 4;
-    for (uint32_t p = threadIdx.x; p < np; p += kThreads) {
-        if (!((dirty[p >> 5] >> (p & 31)) & 1u)) continue;
-        const uint32_t p0 = 16 * p;
+    const unsigned off = (unsigned)((uintptr_t)base & 3u);
+    uint8_t *g = base - off;                                                // image byte 0
+    const int lo = (int)(off + 64u * w * a.dstride),
+              hi = (int)(off + (wend - 1) * a.dstride + a.len + (size_t)b.ecc_bytes);
+    const uint32_t gmis = (uint32_t)((uintptr_t)g & 15u);                  // image offset -> piece grid
+    int last = -1000;
+#pragma unroll
+    for (int i = 0; i < T; ++i) {
+        if (i >= cnt) break;
+        const uint32_t o = (uint32_t)(row - rows) + (loc[i] >> 3);
+        const int p0 = (int)((o + gmis) & ~15u) - (int)gmis;              // image offset of the piece
+        if (p0 == last) continue;
+        last = p0;
         if (p0 >= lo && p0 + 16 <= hi) {
-            *reinterpret_cast<uint4 *>(g + p0) = *reinterpret_cast<const uint4 *>(rows + p0);
+            const uint32_t *s4 = reinterpret_cast<const uint32_t *>(rows + p0);   // dword aligned
+            *reinterpret_cast<uint4 *>(g + p0) = make_uint4(s4[0], s4[1], s4[2], s4[3]);
         } else {
-            for (uint32_t q = p0 < lo ? lo : p0; q < p0 + 16 && q < hi; ++q) g[q] = rows[q];
+            for (int q = p0 < lo ? lo : p0; q < p0 + 16 && q < hi; ++q) g[q] = rows[q];
         }
     }
 }
@@ -490,11 +496,12 @@ __device__ int locate(const DevBch &b, const GF &f, Rem<NW> r, uint32_t nbits,
     return L;
 }
 
-// One codeword of k_bch_decode<T, NW>; with `dirty` (lds_fix) its corrections go to the staged
-// image (row: this lane's row in it) instead of the rows in global memory.
+// One codeword of k_bch_decode<T, NW>; with `fix` (lds_fix) its corrections go to the staged image
+// (row: this lane's row in it) instead of the rows in global memory, and loc[0 .. cnt_out) are
+// left for write_pieces.
 template <int T, int NW>
 __device__ __forceinline__ void decode_one(const DevBch &b, const BchArgs &a, uint8_t *smem, const uint8_t *row,
-                                           size_t k, uint8_t *rows, uint32_t *dirty) {
+                                           size_t k, uint8_t *rows, bool fix, uint32_t (&loc)[T], int &cnt_out) {
     if (8ull * a.len > (unsigned long long)(b.n - b.ecc_bits)) {   // decode_bch's length check
         a.result[k] = -kEINVAL;
         return;
@@ -513,7 +520,7 @@ __device__ __forceinline__ void decode_one(const DevBch &b, const BchArgs &a, ui
         return;
     }
     uint8_t *d = a.ecc_only ? nullptr : a.wdata + k * a.dstride, *e = a.ecc + k * a.estride;
-    const uint8_t *er = dirty ? row + a.len : e;         // the received ECC (staged when inline)
+    const uint8_t *er = fix ? row + a.len : e;           // the received ECC (staged when inline)
     Rem<NW> r;
     if (a.ecc_only) {
 #pragma unroll
@@ -534,16 +541,16 @@ __device__ __forceinline__ void decode_one(const DevBch &b, const BchArgs &a, ui
     for (int i = 0; i < NW; ++i) r.w[i] &= b.emask[i];
     const uint16_t *sx = reinterpret_cast<const uint16_t *>(smem + tabs_offset(b));
     const GF f{b.lds_tabs ? sx : b.ex, b.lds_tabs ? sx + 2 * b.n : b.lg, b.n};
-    uint32_t loc[T];
     const int cnt = locate<T, NW>(b, f, r, 8u * a.len + (uint32_t)b.ecc_bits, loc);
     a.result[k] = cnt;
+    if (fix && cnt > 0) cnt_out = cnt;
 #pragma unroll
     for (int i = 0; i < T; ++i) {
         if (i < cnt) {
             const uint32_t el = loc[i];
             if (a.errloc) a.errloc[k * a.lstride + i] = el;
             if (a.ecc_only) continue;
-            if (dirty) fix_bit_lds(rows, dirty, row, el);
+            if (fix) fix_bit_lds(rows, row, el);
             else if (el < 8u * a.len) d[el >> 3] ^= (uint8_t)(1u << (el & 7));
             else e[(el >> 3) - a.len] ^= (uint8_t)(1u << (el & 7));
         }
@@ -557,11 +564,14 @@ __global__ void __launch_bounds__(kThreads) k_bch_decode(DevBch b, BchArgs a) {
     const uint8_t *row = a.ecc_only ? nullptr : block_rows(smem, b, true, a);
     const size_t k = (size_t)blockIdx.x * kThreads + threadIdx.x;
     uint8_t *rows = smem + rows_offset(b, true);
-    uint32_t *dirty = a.lds_fix ? reinterpret_cast<uint32_t *>(rows + rows_bytes(a)) : nullptr;
-    if (k < a.ncw) decode_one<T, NW>(b, a, smem, row, k, rows, dirty);
+    uint32_t loc[T];
+    int cnt = 0;
+    if (k < a.ncw) decode_one<T, NW>(b, a, smem, row, k, rows, a.lds_fix != 0, loc, cnt);
     if (!a.lds_fix) return;                             // (uniform over the block)
-    __syncthreads();
-    write_back(rows, dirty, b, a);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    write_pieces<T>(rows, row, loc, cnt, b, a);
 }
 
 // ---- t > 16 or ecc_bits > 256: the same decode with run-time t ------------------------------
