@@ -39,6 +39,9 @@ constexpr int32_t kSentinel = INT32_MIN;
 #ifndef EZRS_ERR_STOP
 #define EZRS_ERR_STOP 0                 // timing ablations (variant builds only): see decode_lane
 #endif
+#ifndef EZRS_ERR_BMMASK
+#define EZRS_ERR_BMMASK 1
+#endif
 #ifndef EZRS_ERR_NOCACHE
 #define EZRS_ERR_NOCACHE 0
 #endif
@@ -218,6 +221,33 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
         const unsigned dl = gi(L, discr);
         const bool upd = dl < 510u && 2 * el <= r + no_eras - 1;
         const unsigned ndl = 255u - dl;
+#if EZRS_ERR_BMMASK
+        // lambda += Delta x B only in the lanes whose discrepancy is nonzero: the others issue no
+        // table reads (a zero discrepancy is the rule past step 2 nu + ne of a decodable word)
+        if (dl < 510u) {
+#pragma unroll
+            for (int i0 = 32; i0 >= 0; i0 -= 4) {
+                if ((unsigned)i0 <= umax) {
+#pragma unroll
+                    for (int i = i0 + 3; i >= i0; --i)
+                        if (i > 0 && i <= 32) lam[i] ^= gp(L, (dl + b[i - 1]));
+                }
+            }
+        }
+#pragma unroll
+        for (int i0 = 32; i0 >= 0; i0 -= 4) {
+            if ((unsigned)i0 <= umax) {
+#pragma unroll
+                for (int i = i0 + 3; i >= i0; --i) {
+                    if (i > 32) continue;
+                    const unsigned bp = i > 0 ? b[i - 1] : kZ;
+                    const unsigned d = l[i] + ndl;
+                    const unsigned nb = min(min(d, d - 255u), kZ);
+                    b[i] = upd ? nb : bp;
+                }
+            }
+        }
+#else
 #pragma unroll
         for (int i0 = 32; i0 >= 0; i0 -= 4) {
             if ((unsigned)i0 <= umax) {
@@ -232,6 +262,7 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
                 }
             }
         }
+#endif
         if (dl < 510u) lhi = 0;               // this lane's lambda changed
         el = upd ? r + no_eras - el : el;
     }
