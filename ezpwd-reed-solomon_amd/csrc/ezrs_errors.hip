@@ -39,6 +39,9 @@ constexpr int32_t kSentinel = INT32_MIN;
 #ifndef EZRS_ERR_STOP
 #define EZRS_ERR_STOP 0                 // timing ablations (variant builds only): see decode_lane
 #endif
+#ifndef EZRS_ERR_OMSL
+#define EZRS_ERR_OMSL 1                 // Omega: the syndromes' logs read once into registers
+#endif
 #ifndef EZRS_ERR_BMMASK
 #define EZRS_ERR_BMMASK 1
 #endif
@@ -335,15 +338,24 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
     if (count > 0) {
         // Omega = S * lambda mod x^(deg lambda), index form (1596-1604)
         const unsigned deg_omega = deg - 1;
-        unsigned om[32];
+        unsigned om[32], sl[32];               // sl[k] = log S_k, read once
+#pragma unroll
+        for (int i0 = 0; i0 < 32; i0 += 4) {
+            if ((unsigned)i0 <= deg_omega) {
+#pragma unroll
+                for (int i = i0; i < i0 + 4; ++i) sl[i] = EZRS_ERR_OMSL ? S(31 - i) : 0u;
+            }
+        }
 #pragma unroll
         for (int i0 = 0; i0 < 32; i0 += 4) {
             if ((unsigned)i0 <= deg_omega) {
 #pragma unroll
                 for (int i = i0; i < i0 + 4; ++i) {
                     unsigned t = 0;
+                    if ((unsigned)i <= deg_omega) {      // (lanes past their degree read nothing)
 #pragma unroll
-                    for (int j = 0; j <= i; ++j) t ^= gp(L, (S(31 - (i - j)) + l[j]));
+                        for (int j = 0; j <= i; ++j) t ^= gp(L, ((EZRS_ERR_OMSL ? sl[i - j] : S(31 - (i - j))) + l[j]));
+                    }
                     om[i] = gi(L, t);
                 }
             }
