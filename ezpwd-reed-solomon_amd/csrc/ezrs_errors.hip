@@ -27,9 +27,12 @@
 //    what bounds this kernel (r05j, C3 decode: 0.686 vs 0.731 ms with four positions per read).
 //    Measured and dropped (r05j): corrections applied by the wave in whole 16-byte pieces of the
 //    rows (the records of each row gathered per piece): 1.01 vs 0.73 ms.
-//  * Phase costs on C3 (r05j, timing ablations EZRS_ERR_STOP, whole decode call 0.731 ms, the
-//    syndrome kernel 0.095 of it): screen, syndromes and erasure locator 0.077 ms, Berlekamp-Massey
-//    0.19, Chien 0.22 (four positions per read), Omega and Forney 0.10, applying corrections 0.05.
+//  * Phase costs on C3 (timing ablations EZRS_ERR_STOP; the syndrome kernel is 0.095 ms of the
+//    decode call).  r05j, call 0.731 ms: screen, syndromes and erasure locator 0.077, Berlekamp-
+//    Massey 0.19, Chien 0.22 (four positions per read), Omega and Forney 0.10, corrections 0.05.
+//    r05o, call 0.631 ms (eight positions per read; a codeword's loads issued together; the lambda
+//    update masked to lanes with a nonzero discrepancy; Omega's syndromes read once): 0.05, 0.166,
+//    0.164, 0.103, 0.052.  The LDS -- table reads, half their cycles bank conflicts -- bounds it.
 #include "ezrs_internal.hpp"
 
 namespace ezrs {
@@ -81,7 +84,8 @@ struct Lds {
 
 // Table reads of the decode; gp: the antilog of a sum of two logs (either may be in the zero class).
 // Measured and dropped (C3 decode 0.767 ms): 8-byte antilog reads banked mod 64 (60+ VGPRs of
-// spills), a per-bank replicated antilog table (3 more VALU per read: 0.871 ms), an antilog table
+// spills; again in r05 for every product, conflict-free but 45 VGPRs of spills: 0.722 vs 0.630
+// ms), a per-bank replicated antilog table (3 more VALU per read: 0.871 ms), an antilog table
 // extended over every sum instead of pidx (fewer VALU, more bank conflicts: 0.777 ms), and B
 // updates skipped in wave-uniform branches (170+ VGPRs of spills).
 __device__ __forceinline__ unsigned ga(const Lds &L, unsigned x) { return L.A[x]; }
