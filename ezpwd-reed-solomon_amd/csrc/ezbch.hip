@@ -95,9 +95,11 @@ int want_staging(const DevBch &b, bool tabs, const BchArgs &a) {
            rows_offset(b, tabs) + rows_bytes(a) <= kLdsLimit;
 }
 
-// ECC bytes inline after each row's data (the rows form): the staged image holds them too
+// ECC bytes inline after each row's data, rows packed back to back (the rows form at pitch len +
+// ecc_bytes): the staged image holds them too, and a written-back piece holds no byte outside the
+// rows (a gap between rows is never rewritten)
 int ecc_inline(const DevBch &b, const BchArgs &a) {
-    return a.ecc == a.data + a.len && a.estride == a.dstride && a.dstride >= a.len + (size_t)b.ecc_bytes;
+    return a.ecc == a.data + a.len && a.estride == a.dstride && a.dstride == a.len + (size_t)b.ecc_bytes;
 }
 
 // ---- device ------------------------------------------------------------------------------------

@@ -186,8 +186,14 @@ __device__ int decode_one(const DevCodec &c, const uint16_t *__restrict__ A,
     const bool karn = c.karn != 0, masked = c.masked && !karn;
     if (len == 0 || len > LOAD) return -1;                                    // 1375-1377
     if (no_eras > NR) return -1;                                              // 1380-1382
+    // Karn mode: an erasure outside the frame is reported after the zero-syndrome return, the
+    // order of libfec's checks (decode_rs.h:108-132; -1 here where libfec's result is undefined)
+    bool eras_bad = false;
     for (unsigned i = 0; i < no_eras; ++i)
-        if (eras[i] >= (karn ? NN : len + NR)) return -1;                     // 1383-1387
+        if (eras[i] >= (karn ? NN : len + NR)) {                              // 1383-1387
+            if (!karn) return -1;
+            eras_bad = true;
+        }
     if (masked)
         for (unsigned i = 0; i < NR; ++i)
             if (static_cast<unsigned>(parity[i]) & ~NN) return -1;            // 1215-1218
@@ -243,6 +249,7 @@ __device__ int decode_one(const DevCodec &c, const uint16_t *__restrict__ A,
         syn[(i) * kS] = I[syn[(i) * kS]];
     }
     if (!syn_error) return 0;                                                 // 1427-1434
+    if (eras_bad) return -1;
 
     for (unsigned i = 0; i <= NR; ++i) lambda[(i) * kS] = 0;                        // 1436-1450
     lambda[(0) * kS] = 1;
@@ -364,7 +371,10 @@ __device__ int decode_one(const DevCodec &c, const uint16_t *__restrict__ A,
         if (den == 0 && !karn) { count = -1; goto finish; }
         if (num1 != 0) {
             if (locof(j) < pad) {
-                if (karn) continue;
+                if (karn) {                           // skipped, as libfec does: no correction
+                    if (corr_out) corr_out[j] = static_cast<T>(0);
+                    continue;
+                }
                 count = -1;
                 goto finish;
             }

@@ -96,7 +96,10 @@ int ezrs_kernel_path(const ezrs_codec *codec);
  *     (fec-3.0.1/decode_rs.h:71-298): erasures and positions in the full NN frame (a position
  *     p >= pad is row symbol p - pad), none of those three checks (a zero denominator applies
  *     num1 * num2, a root in the pad is counted and reported but not corrected), the datum is the
- *     symbol.  The Karn ABI (include/ezrs_fec.h) creates its codecs in this mode.
+ *     symbol.  The Karn ABI (include/ezrs_fec.h) creates its codecs in this mode.  As in libfec,
+ *     the syndromes are checked before the erasures: a word with zero syndromes returns 0 even
+ *     with an erasure position >= NN (otherwise -1, where libfec's result is undefined); a root in
+ *     the pad gets correction value 0 in `corr`.
  * Set the semantics once, after create and before the codec's first decode: the setter takes the
  * codec's lock (it waits for a host-memory call in progress), but a device decode already enqueued
  * on a stream runs with the semantics it was launched with, and decodes issued concurrently from

@@ -166,3 +166,70 @@ def test_pad_rs_changes_the_frame(fec):
         assert fec.ezrs_fec_codec(rs)
     finally:
         fec.free_rs_char(rs)
+
+
+@pytest.mark.parametrize("nr", [32, 40])
+def test_karn_erasures_checked_after_syndromes(fec, nr):
+    """Karn mode checks the syndromes before the erasure positions, as libfec's decode_rs does
+    (decode_rs.h:108-132): a clean word with an erasure position >= NN decodes to 0, a corrupted one
+    to -1 (libfec's result is undefined there).  ezpwd mode rejects the position first (-1 for both,
+    rs_base:1383-1387).  NR 32 runs the plane-sliced path, NR 40 the generic one."""
+    import torch
+    import ezrs
+    K = 255 - nr - 20                                   # shortened: pad 20
+    rng = np.random.default_rng(nr)
+    clean = torch.from_numpy(rng.integers(0, 256, (8, K + nr)).astype(np.uint8)).cuda()
+    eras = torch.zeros((8, nr), dtype=torch.int32, device="cuda")
+    eras[:, 0] = 300
+    neras = torch.ones(8, dtype=torch.int32, device="cuda")
+    for mode in ("karn", "ezpwd"):
+        c = ezrs.Codec(8, 0x11d, 1, 1, nr)
+        c.semantics = mode
+        assert c.kernel_path == ("planeslice" if nr == 32 else "generic")
+        c.encode(clean, K)
+        rows = clean.clone()
+        rows[4:, 3] ^= 0x5A                             # rows 4..7 corrupted
+        res = c.decode(rows, K, eras=eras, neras=neras).cpu().numpy()
+        torch.cuda.synchronize()
+        if mode == "karn":
+            np.testing.assert_array_equal(res, [0] * 4 + [-1] * 4)
+        else:
+            np.testing.assert_array_equal(res, [-1] * 8)
+        assert torch.equal(rows[:4], clean[:4])
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c["params"][0] == 8 and c["kind"] != "ccsds"],
+                         ids=lambda c: c["id"])
+def test_device_karn_corrections(fec, case):
+    """Corrections (`corr`) of a Karn-mode device decode: for every root in the data or parity the
+    value XORed into the row (libfec's in/out difference at that position; an entry is left alone
+    where the error value is zero), for a root in the pad (counted but not corrected,
+    decode_rs.h:277-289) zero, or left alone when its error value is zero."""
+    import torch
+    import ezrs
+    m, poly, fcr, prim, nr = case["params"]
+    c = ezrs.Codec(m, poly, fcr, prim, nr)
+    c.semantics = "karn"
+    K = case["data"].shape[1]
+    pad = case["pad"]
+    rows = torch.from_numpy(case["dec_in"].copy()).cuda()
+    eras = torch.from_numpy(case["dec_eras"].astype(np.int32)).cuda()
+    neras = torch.from_numpy(case["dec_neras"].astype(np.int32)).cuda()
+    pos = torch.zeros((rows.shape[0], nr), dtype=torch.int32, device="cuda")
+    corr = torch.full((rows.shape[0], nr), 0xEE, dtype=torch.uint8, device="cuda")
+    res = c.decode(rows, K, None, eras=eras, neras=neras, positions=pos, corr=corr).cpu().numpy()
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(res, case["dec_result"])
+    pos, corr = pos.cpu().numpy().view(np.uint32), corr.cpu().numpy()
+    diff = case["dec_in"] ^ case["dec_out"]
+    npad = 0
+    for k in np.nonzero(res > 0)[0]:
+        for j in range(res[k]):
+            p = int(pos[k, j])                          # full-frame position
+            if p < pad:
+                npad += 1
+                assert corr[k, j] in (0, 0xEE), f"cw {k} root {j} in the pad"
+            else:                                       # (0xEE also: a zero error value, not written)
+                d = diff[k, p - pad]
+                assert corr[k, j] == d or (corr[k, j] == 0xEE and d == 0), f"cw {k} root {j}"
+    print(f"{case['id']}: {int((res > 0).sum())} corrected words, {npad} pad roots")
