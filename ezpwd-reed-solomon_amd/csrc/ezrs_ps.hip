@@ -306,6 +306,18 @@ __device__ __forceinline__ uint32_t row_at(const PsArgs &a, uint32_t k, int &lo)
     return q * a.spitch + j * a.stride;
 }
 
+// A shard tile's DMA start moved down to the 16-byte grid (its image then begins up to 15 bytes
+// early; the row table's offsets are taken from the same start): the 1 KiB LDS-DMA pieces of a
+// tile that starts mid-row are otherwise misaligned 16-byte loads, each split in the memory
+// pipeline (r05r: 1 MiB shards decode 114.7 us against 80.2 us for a plain batch of as many
+// codewords).  Kept as is when the widened span would pass the image.
+__device__ __forceinline__ uint32_t sh_align(uint32_t off, uint32_t &bytes) {
+    const uint32_t mis = off & 15u;
+    if (bytes + mis > (uint32_t)kImage) return off;
+    bytes += mis;
+    return off - mis;
+}
+
 __device__ __forceinline__ void issue_tile_lin(uint32_t lbuf, pw_rsrc_t rsrc, uint32_t toff, uint32_t tile_bytes,
                                                int w, int ablate) {
     if (ablate & 8) return;
@@ -568,7 +580,7 @@ __device__ __forceinline__ void pt_run_lin(const PsArgs &a, uint8_t *lds) {
         int lo;
         const uint32_t t0 = t * kTile, off = row_at(a, t0, lo);
         bytes = (t0 + kTile < a.ncw ? row_at(a, t0 + kTile, lo) : a.span) - off;
-        return off;
+        return sh_align(off, bytes);
     };
     uint32_t tile = blockIdx.x;
     uint32_t tbytes, toff = tile < a.ntiles ? tile_range(tile, tbytes) : 0u;
@@ -1165,7 +1177,7 @@ __device__ __forceinline__ void pq_run(const PsArgs &a, uint8_t *lds) {
         int lo;
         const uint32_t t0 = t * kTile, off = pt::row_at(a, t0, lo);
         bytes = (t0 + kTile < a.ncw ? pt::row_at(a, t0 + kTile, lo) : a.span) - off;
-        return off;
+        return pt::sh_align(off, bytes);
     };
     uint32_t tile = blockIdx.x;
     PQ_RT(0);
