@@ -5,6 +5,7 @@
 // points validate arguments the way the reference's encode<INP>/decode<INP> do
 // (rs_base:868-904, 1170-1242) and dispatch to the fastest kernel that is bit-exact for the codec:
 // the bit-sliced GF(2^8) kernels where they apply, the generic per-codeword kernels otherwise.
+#include <atomic>
 #include <cerrno>
 #include <cstdlib>
 #include <cstdio>
@@ -35,6 +36,7 @@ struct ezrs_codec {
     int bs_id = -1;               // bit-sliced GF(2^8) kernel set, -1 if none
     int ps_id = -1;               // plane-sliced GF(2^8) kernel set, -1 if none
     int wide_id = -1;             // GF(2^16) remainder kernel set, -1 if none
+    mutable std::atomic<uint32_t> decode_gen{0};   // plane-sliced decode calls (DecodeArgs::flag_gen)
     std::vector<uint16_t> wide_blob;   // host: leader slots | log beta | column tables
     uint16_t *d_wcols = nullptr;  // device copy of the column tables (constant multipliers)
     // Device workspaces of the batch entry points, one per HIP stream: calls on different streams
@@ -269,7 +271,7 @@ namespace {
 size_t ws_bytes_for(const ezrs_codec *c, size_t ncw) {
     size_t b = 0;                                          // both >= ncw * 32 (decode's need)
     if (c->bs_id >= 0) b = bs_encode_ws_bytes(ncw);
-    if (c->ps_id >= 0 && ps_ws_bytes(ncw) > b) b = ps_ws_bytes(ncw);
+    if (c->ps_id >= 0 && ps_ws_bytes(ncw) + 256 > b) b = ps_ws_bytes(ncw) + 256;   // + the flag word
     if (c->wide_id >= 0 && wide_ws_bytes(c->wide_id, ncw) > b) b = wide_ws_bytes(c->wide_id, ncw);
     return b;
 }
@@ -313,8 +315,13 @@ hipError_t dispatch_decode(const ezrs_codec *c, const DecodeArgs &a, uint8_t *sy
     const bool contiguous = a.parity == static_cast<char *>(a.data) + (size_t)a.len * w &&
                             a.parity_stride == a.data_stride;
     if (c->ps_id >= 0 && ps_can_decode(c->dev, a)) {
-        hipError_t e = launch_ps_syndromes(c->ps_id, c->dev, a, syn_ws, st);
-        if (e == hipSuccess) e = launch_decode_flagged(c->dev, a, syn_ws, SynLayout::Tiled, st);
+        // the call's flag word (after the tiled syndromes) and a value no earlier call stored there
+        // (a stale match only costs the error path's full screen)
+        DecodeArgs b = a;
+        b.flag_word = reinterpret_cast<uint32_t *>(syn_ws + ps_ws_bytes(a.ncw));
+        b.flag_gen = c->decode_gen.fetch_add(1, std::memory_order_relaxed) + 1;
+        hipError_t e = launch_ps_syndromes(c->ps_id, c->dev, b, syn_ws, st);
+        if (e == hipSuccess) e = launch_decode_flagged(c->dev, b, syn_ws, SynLayout::Tiled, st);
         return e;
     }
     if (a.sh.rows) return launch_decode_generic(c->dev, a, st);     // shard rows: per-codeword kernels

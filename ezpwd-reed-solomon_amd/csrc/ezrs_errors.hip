@@ -498,6 +498,8 @@ __global__ void __launch_bounds__(64 * kWaves) k_decode_errors(DevCodec c, Decod
                                                               SynLayout layout) {
     __shared__ __attribute__((aligned(16))) Lds L;
     const unsigned lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // nothing flagged by this call's syndrome kernel and no erasures: no screen (C2 decode)
+    if (a.flag_word && !a.neras && *reinterpret_cast<volatile const uint32_t *>(a.flag_word) != a.flag_gen) return;
     const size_t nspan = (a.ncw + kSpan - 1) / kSpan, step = (size_t)gridDim.x * kWaves;
     unsigned any = 0;
     for (size_t sp = (size_t)blockIdx.x * kWaves + wave; sp < nspan; sp += step)

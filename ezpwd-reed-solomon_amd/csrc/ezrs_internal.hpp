@@ -87,6 +87,11 @@ struct DecodeArgs {
     size_t corr_stride;
     size_t ncw;
     Shards sh{};                  // sh.rows != 0: shard rows, parity inline (data + row length)
+    // plane-sliced path: the syndrome kernel stores flag_gen into *flag_word when it flags a
+    // codeword, and the error path skips its screen when the word holds another value (and no
+    // erasures are given): nothing was flagged by this call
+    uint32_t *flag_word = nullptr;
+    uint32_t flag_gen = 0;
 };
 
 struct EncodeArgs {

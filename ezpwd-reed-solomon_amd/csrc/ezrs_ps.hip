@@ -113,6 +113,8 @@ struct PsArgs {
     uint32_t spitch;            // shard pitch in bytes
     int ablate;                 // timing experiments only (tools/pt_ablate.py, EZRS_PT_ABLATE): bit 0
                                 // no main loop, 1 no exchange, 2 no fold, 3 no DMA, 5 nothing flagged
+    uint32_t *flag;             // decode: gen stored here when a codeword is flagged (DecodeArgs)
+    uint32_t gen;
 };
 
 template <int I, int N, class F> __device__ __forceinline__ void static_for(F &&f) {
@@ -533,6 +535,7 @@ __device__ __forceinline__ void wave_tail_lin(uint32_t (&V)[C::NI][8], const PsA
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 store_dword(rout, (cw0 + k) * 4u, (fl >> k & 1) ? (uint32_t)kSentinel : 0u);
+            if (fl != 0 && a.flag) *a.flag = a.gen;          // this call flagged a codeword
         }
         if (__ballot(fl != 0) != 0) {                        // flagged codewords: their syndromes
             transpose8(Qs);                                  // Qs[jj] byte k: syndrome jj, codeword k
@@ -1135,6 +1138,7 @@ __device__ __forceinline__ void wave_tail(uint32_t (&V)[C::NI][8], const PsArgs 
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 pt::store_dword(rout, (cw0 + k) * 4u, (fl >> k & 1) ? (uint32_t)kSentinel : 0u);
+            if (fl != 0 && a.flag) *a.flag = a.gen;          // this call flagged a codeword
         }
         if (__ballot(fl != 0) != 0) {                        // flagged codewords: their syndromes
             static_for<0, C::NQ>([&](auto qc) {
@@ -1537,6 +1541,7 @@ __device__ __forceinline__ void wave_run(const PsArgs &a, uint8_t *lds) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
                     pt::store_dword(rout, (cw0 + k) * 4u, (fl >> k & 1) ? (uint32_t)kSentinel : 0u);
+                if (fl != 0 && a.flag) *a.flag = a.gen;      // this call flagged a codeword
             }
             prev_flagged = __ballot(fl != 0) != 0;           // wave-uniform (the same for all waves)
             if (prev_flagged) {                              // flagged codewords: their syndromes
@@ -2054,6 +2059,8 @@ hipError_t launch_ps_syndromes(int id, const DevCodec &d, const DecodeArgs &a, u
         p.ws = syn_ws + k0 / 256 * kSynTile;                  // tiled layout, global codeword index
         p.ws_pitch = k0 % 256;
         p.ablate = pt_ablate();
+        p.flag = a.flag_word;
+        p.gen = a.flag_gen;
         const unsigned grid = syn_grid(d, p.ntiles);
         int k = 0;
 #define EZRS_PS_SYN(C)                                                                            \
