@@ -52,6 +52,8 @@ struct DevBch {
     const uint64_t *step;     // [256][nw] byte-step remainder table
     const uint16_t *ex;       // [2n] alpha^i
     const uint16_t *lg;       // [n+1] log_alpha (lg[0] unused)
+    const uint64_t *syn_tab;  // ecc_bits <= 64, t <= 4: [8][256] the odd syndromes S1, S3, S5, S7
+                              // (16 bits each) of remainder byte b (from the top) holding value v
 };
 
 struct BchArgs {
@@ -388,8 +390,19 @@ __device__ int locate(const DevBch &b, const GF &f, Rem<NW> r, uint32_t nbits,
         for (int j = 1; j <= 2 * T; ++j) bad |= S[j] > n;
         if (bad) return -EINVAL;
     }
+    bool tab = false;
+    if constexpr (NW == 1 && T <= 4) {
+        if (b.syn_tab && !sin) {            // the odd syndromes are GF(2)-linear in the remainder's
+            tab = true;                     // bits: one table entry per remainder byte
+            uint64_t acc = 0;
+            for (int bb = 0; bb < b.ecc_bytes; ++bb)
+                acc ^= b.syn_tab[bb * 256 + (uint32_t)((r.w[0] >> (56 - 8 * bb)) & 255u)];
 #pragma unroll
-    for (int wi = 0; wi < NW && !sin; ++wi) {
+            for (int j = 1; j < 2 * T; j += 2) S[j] = (uint32_t)(acc >> (8 * (j - 1))) & 0xFFFFu;
+        }
+    }
+#pragma unroll
+    for (int wi = 0; wi < NW && !sin && !tab; ++wi) {
         uint64_t x = r.w[wi];
         while (x) {                         // S_j = r(alpha^j), j odd
             const int lz = __clzll(x);
@@ -1230,6 +1243,7 @@ struct ezbch_codec {
     DevBch dev{};
     uint64_t *d_step = nullptr;
     uint16_t *d_tabs = nullptr;
+    uint64_t *d_syn = nullptr;    // DevBch::syn_tab
     std::mutex mu;                // guards the host-pipeline buffers
     void *d_stage = nullptr;
     size_t stage_bytes = 0;
@@ -1292,6 +1306,26 @@ int create_impl(ezbch_codec **out, unsigned m, unsigned t, unsigned poly, int de
     d.step = c->d_step;
     d.ex = c->d_tabs;
     d.lg = c->d_tabs + c->h.ex.size();
+    if (!d.nwl && d.nw == 1 && t <= 4) {    // syndrome byte tables (locate<T, 1>)
+        std::vector<uint64_t> st(8 * 256, 0);
+        const unsigned n = c->h.n, eb = c->h.ecc_bits;
+        for (unsigned bb = 0; bb < 8; ++bb)
+            for (unsigned v = 0; v < 256; ++v)
+                for (unsigned i = 0; i < 8; ++i) {
+                    if (!(v >> i & 1)) continue;
+                    const unsigned lz = 63 - (56 - 8 * bb + i);      // the bit's leading-zero index
+                    if (lz >= eb) continue;                           // masked (unused ECC bits)
+                    const unsigned p = eb - 1 - lz;                   // S_j += alpha^(j p)
+                    for (unsigned j = 1; j < 2 * t; j += 2)
+                        st[bb * 256 + v] ^= (uint64_t)c->h.ex[(uint64_t)j * p % n] << (8 * (j - 1));
+                }
+        if ((e = hipMalloc(&c->d_syn, st.size() * 8)) != hipSuccess ||
+            (e = hipMemcpy(c->d_syn, st.data(), st.size() * 8, hipMemcpyHostToDevice)) != hipSuccess) {
+            ezbch_destroy(c);
+            return hip_fail(e, "BCH syndrome tables");
+        }
+        d.syn_tab = c->d_syn;
+    }
     *out = c;
     return 0;
 }
@@ -1359,6 +1393,7 @@ int ezbch_destroy(ezbch_codec *c) {
     DeviceGuard g(c->device);
     if (c->d_step) (void)hipFree(c->d_step);
     if (c->d_tabs) (void)hipFree(c->d_tabs);
+    if (c->d_syn) (void)hipFree(c->d_syn);
     if (c->d_stage) (void)hipFree(c->d_stage);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->stream) (void)hipStreamDestroy(c->stream);
