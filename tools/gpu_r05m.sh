@@ -1,9 +1,9 @@
 #!/bin/bash
-# r05u: BCH GPU tests on the default library (per-wave write-back of LDS corrections), then C5 timing
+# r05w: BCH GPU tests on the default library (per-wave write-back of LDS corrections), then C5 timing
 # A/B: default vs block-barrier write-back (bblk) vs global byte corrections (bold), 1M and 8M.
 set -u
 cd $GRAFT_REPO_ROOT
-OUT=gpurun_out/r05u; mkdir -p $OUT
+OUT=gpurun_out/r05w; mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "bch or BCH or host" > $OUT/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -n 2 $OUT/pytest.log; [ $rc -eq 0 ] || exit $rc
