@@ -2,7 +2,7 @@
 # r05p: the final round-5 tree -- GPU suite, smoke, the driver's bench line, a K = 200 line, kernel
 # traces (C2, C3, C5 at 1M and 8M) and FETCH / WRITE passes (C3, C5 at 8M), one counter per run.
 set -u
-TAG=${1:-r05p}; OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG; mkdir -p $OUT
+TAG=${1:-r05x}; OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG; mkdir -p $OUT
 export TMPDIR=/tmp
 run() {  # name timeout cmd...
   local name=$1 to=$2; shift 2
