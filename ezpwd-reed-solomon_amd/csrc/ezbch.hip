@@ -433,6 +433,54 @@ __device__ int locate(const DevBch &b, const GF &f, Rem<NW> r, uint32_t nbits,
         B[j] = j == 1;
     }
     int L = 0;
+#ifndef EZRS_BCH_BM_LOG
+#define EZRS_BCH_BM_LOG 1
+#endif
+#if EZRS_BCH_BM_LOG
+    // Log domain: the syndromes' logs once (an even one is twice the log of its half), the
+    // discrepancy's quotient by its log, and only the coefficients that can be nonzero: before odd
+    // step rr, deg C <= rr - 1 and deg B <= rr (B = x at rr = 1; C + q B, x^2 C, x^2 B keep it),
+    // so the update touches C[1..rr].
+    constexpr uint32_t kNoLog = 0xFFFFu;
+    uint32_t lS[2 * T + 1];
+#pragma unroll
+    for (int j = 1; j <= 2 * T; ++j) {
+        if (j % 2 || sin) {                 // a caller's even syndromes are taken as given
+            lS[j] = S[j] ? (uint32_t)f.lg[S[j]] : kNoLog;
+        } else {
+            const uint32_t h = lS[j / 2];
+            lS[j] = h == kNoLog ? kNoLog : (2 * h >= n ? 2 * h - n : 2 * h);
+        }
+    }
+    uint32_t lbd = 0;                       // log of the last nonzero discrepancy (bd = 1)
+#pragma unroll
+    for (int rr = 1; rr < 2 * T; rr += 2) {
+        uint32_t d = S[rr];
+#pragma unroll
+        for (int i = 1; i < rr; ++i)
+            if (C[i] && lS[rr - i] != kNoLog) d ^= f.ex[f.lg[C[i]] + lS[rr - i]];
+        if (d) {
+            const bool grow = 2 * L <= rr - 1;
+            const uint32_t ld = f.lg[d];
+            const uint32_t lq = ld >= lbd ? ld - lbd : ld + n - lbd;    // log (d / bd)
+            uint32_t old[W];
+#pragma unroll
+            for (int j = 0; j < W; ++j) old[j] = C[j];
+#pragma unroll
+            for (int j = 1; j <= rr && j < W; ++j)
+                if (B[j]) C[j] ^= f.ex[lq + f.lg[B[j]]];
+            if (grow) {
+                L = rr - L;
+                lbd = ld;
+            }
+#pragma unroll
+            for (int j = W - 1; j >= 0; --j) B[j] = j >= 2 ? (grow ? old[j - 2] : B[j - 2]) : 0u;
+        } else {
+#pragma unroll
+            for (int j = W - 1; j >= 0; --j) B[j] = j >= 2 ? B[j - 2] : 0u;
+        }
+    }
+#else
     uint32_t bd = 1;
 #pragma unroll
     for (int rr = 1; rr < 2 * T; rr += 2) {
@@ -459,6 +507,7 @@ __device__ int locate(const DevBch &b, const GF &f, Rem<NW> r, uint32_t nbits,
             for (int j = W - 1; j >= 0; --j) B[j] = j >= 2 ? B[j - 2] : 0u;
         }
     }
+#endif
     if (L > T) return -kEBADMSG;
     if (L == 0) return 0;
     uint32_t lead = 0;

@@ -1828,6 +1828,40 @@ __global__ void __launch_bounds__(512) k_ps_parity8(const uint8_t *ws, size_t ws
     __syncthreads();
     PAR_STAMP(6);
     const size_t cwb = g0 * 32;
+    // two lanes per parity row, NR / 2 bytes each (NR % 8 == 0): a wave's store covers 32 rows
+    // instead of 64 (C2 line 1549 vs 1526 GB/s; 4 or 8 lanes per row the same within noise,
+    // r05y / r05z A/B); other NR: one lane per row
+#ifndef EZRS_PAR_LPR
+#define EZRS_PAR_LPR 2
+#endif
+    if constexpr (NR % (4 * EZRS_PAR_LPR) == 0) {
+        constexpr int LPR = EZRS_PAR_LPR, PB = NR / LPR;
+        const int sub = threadIdx.x % LPR;
+        for (int r = threadIdx.x / LPR; r < kParCw; r += 512 / LPR) {
+            const size_t k = cwb + r;
+            if (k >= ncw) break;
+            unsigned rlen;
+            uint8_t *dst = sh.rows ? parity + shard_row(sh, k, pstride, len, rlen) + rlen : parity + k * pstride;
+            const uint8_t *s8 = stage + (r >> 5) * kRegion + (r & 31) * NR + PB * sub;
+            if constexpr (PB == 16) {
+                const uint2 lo = *reinterpret_cast<const uint2 *>(s8);      // the stage is 8-aligned
+                const uint2 hi = *reinterpret_cast<const uint2 *>(s8 + 8);
+                const pt::u32x4 v = {lo.x, lo.y, hi.x, hi.y};
+                __builtin_memcpy(dst + PB * sub, &v, 16);
+            } else if constexpr (PB % 8 == 0) {
+#pragma unroll
+                for (int o = 0; o < PB; o += 8) {
+                    uint2 v = *reinterpret_cast<const uint2 *>(s8 + o);
+                    __builtin_memcpy(dst + PB * sub + o, &v, 8);
+                }
+            } else {
+                uint32_t v = *reinterpret_cast<const uint32_t *>(s8);
+                __builtin_memcpy(dst + PB * sub, &v, 4);
+            }
+        }
+        PAR_STAMP(7);
+        return;
+    }
     for (int r = threadIdx.x; r < kParCw; r += 512) {
         const size_t x = cwb + r;
         const size_t k = x;
