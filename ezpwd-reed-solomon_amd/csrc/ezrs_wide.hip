@@ -364,7 +364,10 @@ struct ErrArgs {
     uint16_t qsolve[16];        // y = sum_j c_j qsolve[j] solves y^2 + y = c when Tr(c) = 0
 };
 
-constexpr int kErrWaves = 16;
+#ifndef EZRS_WIDE_ERR_WAVES
+#define EZRS_WIDE_ERR_WAVES 16
+#endif
+constexpr int kErrWaves = EZRS_WIDE_ERR_WAVES;
 // per-wave scratch, dwords: roots 64, omega/syndromes/lambda 3 x 32, factor pool 32 (64 u16),
 // factor stack 40
 constexpr int kErrScratch = 64 + 3 * 32 + 32 + 40;
