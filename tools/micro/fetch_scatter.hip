@@ -1,0 +1,119 @@
+// FETCH_SIZE / WRITE_SIZE calibration for scattered accesses (the C3 error kernel's pattern), to set
+// against the x2 FETCH correction that tools/micro/ps_stream2 calibrated on wide streaming reads.
+// Run each counter in its own rocprofv3 --pmc pass; the program prints the bytes each kernel must
+// move at 32-, 64- and 128-byte granularity so the counters can be read against them.
+//   k_stream : 1 GiB read linearly, 16-byte loads, coalesced
+//   k_lines<G>: N distinct random 128-byte lines of a 4 GiB buffer, G bytes read from each line's start
+//   k_rows12 : C3's correction pattern -- 1 M rows at pitch 255, 12 distinct random byte positions per
+//              row, each a byte read-modify-write (XOR)
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+#include <vector>
+#include <set>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
+
+__global__ void k_stream(const uint4 *p, size_t n16, unsigned *out) {
+    unsigned acc = 0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x) {
+        const uint4 v = p[i];
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (acc == 0x9E3779B9u) out[0] = acc;                 // keeps the loads; never true for the fill
+}
+
+__device__ __forceinline__ uint32_t mix(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+    return x;
+}
+
+template <int G>
+__global__ void k_lines(const uint8_t *p, uint32_t nlines_total, uint32_t n, unsigned *out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t line = (uint32_t)(((uint64_t)i * 2654435761u) & (nlines_total - 1));  // odd multiplier: distinct
+    const uint8_t *q = p + (size_t)line * 128;
+    unsigned acc = 0;
+    if constexpr (G == 1) acc = q[0];
+    else if constexpr (G == 16) { const uint4 v = *reinterpret_cast<const uint4 *>(q); acc = v.x ^ v.y ^ v.z ^ v.w; }
+    else {
+#pragma unroll
+        for (int k = 0; k < G / 16; ++k) { const uint4 v = reinterpret_cast<const uint4 *>(q)[k]; acc ^= v.x ^ v.y ^ v.z ^ v.w; }
+    }
+    if (acc == 0x9E3779B9u) out[0] = acc;
+}
+
+__device__ __forceinline__ void row_positions(uint32_t r, uint32_t (&pos)[12]) {
+    uint32_t h = mix(r * 0x9E3779B1u + 1);
+    int n = 0;
+    while (n < 12) {
+        h = mix(h + 0x632BE5ABu);
+        const uint32_t p = h % 255u;
+        bool dup = false;
+        for (int k = 0; k < n; ++k) dup |= pos[k] == p;
+        if (!dup) pos[n++] = p;
+    }
+}
+
+__global__ void k_rows12(uint8_t *rows, uint32_t nrows) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nrows) return;
+    uint32_t pos[12];
+    row_positions(r, pos);
+    uint8_t *row = rows + (size_t)r * 255;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) row[pos[k]] ^= (uint8_t)(1u + k);
+}
+
+static uint32_t mix_h(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+    return x;
+}
+
+int main() {
+    const size_t big = (size_t)4 << 30, s1 = (size_t)1 << 30;
+    uint8_t *buf;
+    unsigned *out;
+    CK(hipMalloc(&buf, big));
+    CK(hipMalloc(&out, 64));
+    CK(hipMemset(buf, 0x5A, big));
+    CK(hipDeviceSynchronize());
+    // streaming
+    k_stream<<<4096, 256>>>(reinterpret_cast<const uint4 *>(buf), s1 / 16, out);
+    printf("k_stream: %zu bytes read linearly\n", s1);
+    // scattered lines
+    const uint32_t nl = (uint32_t)(big / 128), n = 8u << 20;
+    k_lines<1><<<(n + 255) / 256, 256>>>(buf, nl, n, out);
+    k_lines<16><<<(n + 255) / 256, 256>>>(buf, nl, n, out);
+    k_lines<64><<<(n + 255) / 256, 256>>>(buf, nl, n, out);
+    printf("k_lines<G>: %u distinct lines; bytes at 32/64/128 B granules: %.1f / %.1f / %.1f MB "
+           "(G = 1, 16: one 32 B granule; G = 64: two)\n", n, n * 32 / 1e6, n * 64 / 1e6, n * 128 / 1e6);
+    // C3's correction pattern
+    const uint32_t nr = 1u << 20;
+    k_rows12<<<(nr + 255) / 256, 256>>>(buf, nr);
+    CK(hipDeviceSynchronize());
+    std::set<uint64_t> g32, g64, g128;
+    for (uint32_t r = 0; r < nr; ++r) {
+        uint32_t pos[12];
+        uint32_t h = mix_h(r * 0x9E3779B1u + 1);
+        int m = 0;
+        while (m < 12) {
+            h = mix_h(h + 0x632BE5ABu);
+            const uint32_t p = h % 255u;
+            bool dup = false;
+            for (int k = 0; k < m; ++k) dup |= pos[k] == p;
+            if (!dup) pos[m++] = p;
+        }
+        for (int k = 0; k < 12; ++k) {
+            const uint64_t a = (uint64_t)r * 255 + pos[k];
+            g32.insert(a >> 5); g64.insert(a >> 6); g128.insert(a >> 7);
+        }
+    }
+    printf("k_rows12: %u rows x 12 byte RMWs; distinct granules touched: 32 B %.1f MB, 64 B %.1f MB, "
+           "128 B %.1f MB (each read and written)\n", nr, g32.size() * 32 / 1e6, g64.size() * 64 / 1e6,
+           g128.size() * 128 / 1e6);
+    CK(hipFree(buf));
+    CK(hipFree(out));
+    return 0;
+}
