@@ -35,7 +35,7 @@ __global__ void k_lines(const uint8_t *p, uint32_t nlines_total, uint32_t n, uns
     const uint32_t line = (uint32_t)(((uint64_t)i * 2654435761u) & (nlines_total - 1));  // odd multiplier: distinct
     const uint8_t *q = p + (size_t)line * 128;
     unsigned acc = 0;
-    if constexpr (G == 1) acc = q[0];
+    if constexpr (G == 1) acc = q[0] == 0x77u ? 0x9E3779B9u : 0u;   // (a byte alone never equals the sentinel)
     else if constexpr (G == 16) { const uint4 v = *reinterpret_cast<const uint4 *>(q); acc = v.x ^ v.y ^ v.z ^ v.w; }
     else {
 #pragma unroll
