@@ -208,6 +208,19 @@ __device__ __forceinline__ void barrier() { asm volatile("s_barrier" ::: "memory
 __device__ __forceinline__ void store_dword(pw_rsrc_t r, uint32_t off, uint32_t v) {
     asm volatile("buffer_store_dword %0, %1, %2, 0 offen" :: "v"(v), "v"(off), "s"(r) : "memory");
 }
+// A/B (EZRS_SYN_POLICY): the encode syndrome workspace stores with a cache policy -- 1 nt, 2 sc1,
+// 3 sc0 sc1 -- to see whether the dirty lines the next launch waits on set the gap between them
+__device__ __forceinline__ void store_dword_syn(pw_rsrc_t r, uint32_t off, uint32_t v) {
+#if defined(EZRS_SYN_POLICY) && EZRS_SYN_POLICY == 1
+    asm volatile("buffer_store_dword %0, %1, %2, 0 offen nt" :: "v"(v), "v"(off), "s"(r) : "memory");
+#elif defined(EZRS_SYN_POLICY) && EZRS_SYN_POLICY == 2
+    asm volatile("buffer_store_dword %0, %1, %2, 0 offen sc1" :: "v"(v), "v"(off), "s"(r) : "memory");
+#elif defined(EZRS_SYN_POLICY) && EZRS_SYN_POLICY == 3
+    asm volatile("buffer_store_dword %0, %1, %2, 0 offen sc0 sc1" :: "v"(v), "v"(off), "s"(r) : "memory");
+#else
+    store_dword(r, off, v);
+#endif
+}
 __device__ __forceinline__ void store_byte(pw_rsrc_t r, uint32_t off, uint32_t v) {
     asm volatile("buffer_store_byte %0, %1, %2, 0 offen" :: "v"(v), "v"(off), "s"(r) : "memory");
 }
@@ -1113,7 +1126,7 @@ __device__ __forceinline__ void wave_tail(uint32_t (&V)[C::NI][8], const PsArgs 
 #pragma unroll
             for (int jj = 0; jj < 4; ++jj)
                 if (C::SYN[W][qd][jj] >= 0)
-                    pt::store_dword(rws, (uint32_t)(C::SYN[W][qd][jj] * a.ws_pitch) + cw0, Qs[qd][jj]);
+                    pt::store_dword_syn(rws, (uint32_t)(C::SYN[W][qd][jj] * a.ws_pitch) + cw0, Qs[qd][jj]);
         });
     } else {
         uint32_t fl = 0;
@@ -1516,7 +1529,7 @@ __device__ __forceinline__ void wave_run(const PsArgs &a, uint8_t *lds) {
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj)
                     if (C::SYN[W][qd][jj] >= 0)
-                        pt::store_dword(rws, (uint32_t)(C::SYN[W][qd][jj] * a.ws_pitch) + cw0, Qs[qd][jj]);
+                        pt::store_dword_syn(rws, (uint32_t)(C::SYN[W][qd][jj] * a.ws_pitch) + cw0, Qs[qd][jj]);
             });
         } else {
             uint32_t fl = 0;
