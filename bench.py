@@ -571,6 +571,17 @@ def timed_pair(enc_fn, dec_fn, steps, warmup, pre=None):
             sum(e[1].elapsed_time(e[2]) for e in evs) / steps)
 
 
+def uniform_positions(gen, rows, n, m, rows_per_chunk=1 << 17):
+    """[rows, m] int64: per row m distinct positions drawn uniformly from [0, n) (the indices of the
+    m largest of n uniform draws: a uniformly random m-subset in random order), on the device."""
+    import torch
+    out = torch.empty((rows, m), dtype=torch.int64, device="cuda")
+    for r0 in range(0, rows, rows_per_chunk):
+        nr = min(rows_per_chunk, rows - r0)
+        out[r0:r0 + nr] = torch.rand((nr, n), generator=gen, device="cuda").topk(m, dim=1).indices
+    return out
+
+
 def c4_extra(gen, steps=3):
     """SURVEY 8(d) C4 on the default line: RS(65535,65503), 65 536 codewords (8.6 GB of 16-bit
     symbols, BASELINE configs[3], rsexercise.C:27-28), each with 12 distinct corrupted symbols of
@@ -586,11 +597,7 @@ def c4_extra(gen, steps=3):
                                             device="cuda", dtype=torch.int16)
     u16 = clean.view(torch.uint16)
     c.encode(u16, k)
-    units = [s for s in (1, 2, 4, 7, 8, 11, 13, 14, 16, 19, 22, 23, 26, 28, 29, 31) if s % 3 and s % 5]
-    cop = torch.tensor(units, device="cuda")
-    b0 = torch.randint(0, n, (ncw, 1), generator=gen, device="cuda")
-    st = cop[torch.randint(0, len(units), (ncw, 1), generator=gen, device="cuda")]
-    locs = (b0 + torch.arange(12, device="cuda")[None, :] * st) % n     # 12 distinct positions
+    locs = uniform_positions(gen, ncw, n, 12, rows_per_chunk=2048)   # distinct, uniform
     vals = torch.randint(1, 65536, (ncw, 12), generator=gen, device="cuda", dtype=torch.int32).to(torch.int16)
     master = clean.clone()
     master.scatter_(1, locs, master.gather(1, locs) ^ vals)
@@ -691,16 +698,13 @@ def c2_extras(codec, args):
     log(f"extras: c2_4m {out['c2_4m']}")
     del big, res4
     torch.cuda.empty_cache()
-    # C3: 1M codewords, 12 distinct corrupted symbols (positions b + j s mod 255, s coprime to 255),
-    # the last 4 passed as erasures; the corrupted master is copied in before each step (outside
-    # the events)
+    # C3: 1M codewords, 12 distinct corrupted symbols at positions uniform over [0, 255) (SURVEY
+    # 8(d)), the last 4 passed as erasures; the corrupted master is copied in before each step
+    # (outside the events)
     ncw = 1 << 20
     clean = torch.randint(0, 256, (ncw, N), generator=gen, device="cuda", dtype=torch.int32).to(torch.uint8)
     codec.encode(clean, K)
-    cop = torch.tensor([s_ for s_ in range(1, 255) if np.gcd(s_, 255) == 1], device="cuda")
-    b0 = torch.randint(0, 255, (ncw, 1), generator=gen, device="cuda")
-    st_ = cop[torch.randint(0, len(cop), (ncw, 1), generator=gen, device="cuda")]
-    locs = (b0 + torch.arange(12, device="cuda")[None, :] * st_) % 255
+    locs = uniform_positions(gen, ncw, N, 12)
     vals = torch.randint(1, 256, (ncw, 12), generator=gen, device="cuda", dtype=torch.int32).to(torch.uint8)
     master = clean.clone()
     master.scatter_(1, locs, master.gather(1, locs) ^ vals)
@@ -971,6 +975,13 @@ def main():
             line["e2e_host_gbs"] = e2e
         if extras is not None:
             line.update(extras)
+            # the dominant call's fraction past the 256 MiB Infinity Cache: the same calls on 4 M
+            # codewords (1.07 GB) in this run, the HBM figure (the 1 M batch is 267 MB, which the
+            # L3 partly serves)
+            c4m = extras["c2_4m"]
+            roofline["past_l3"] = {"codewords": c4m["codewords"],
+                                   "frac_encode": c4m["frac_encode"], "frac_decode": c4m["frac_decode"],
+                                   "frac": c4m["frac_encode"] if dom == "ezrs_encode" else c4m["frac_decode"]}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

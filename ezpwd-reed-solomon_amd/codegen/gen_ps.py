@@ -17,8 +17,8 @@ and the others follow by squaring in the epilogue.
 Main loop (tile kernel k_pt, PT_<codec>).  Per 8 positions and leader bit q the state word takes
 one 3-input XOR of two Four-Russians combinations (all 15 XORs of four position words are formed
 once per 4 positions).  A workgroup of 8 waves covers a tile of 256 codewords (4 per lane): wave
-(g, q) evaluates leader group g over the 16-position pieces of quarter q with quarter 0's networks,
-then fixes its partials up by alpha^(-16 q e) and a recursive-halving exchange sums them.
+(g, q) evaluates leader group g over the 16-position pieces of quarter q, each piece with its own
+networks, and a recursive-halving exchange sums the quarters' partials.
 
 Epilogue: expansion (squarings) and the plane fold S = sum_b alpha^b V_b inside each byte (3
 levels: x alpha, x alpha^2, x alpha^4 with shifts 1,2,4), four syndromes packed per word.
@@ -500,11 +500,9 @@ class PtRole:
 def gen_pt(c: PsCodec):
     """Tile-kernel tables and straight-line code, PT_<codec>: syndromes by coset leaders, the
     leaders split into GN groups, the positions into QN quarters.  Wave (g, q) reads pieces
-    q, q + QN, q + 2 QN, ... and runs the networks of quarter 0's pieces on them -- so one network
-    set per group serves every quarter and the kernel's code stays small enough for the
-    instruction cache -- then multiplies its partials by alpha^(-16 q e) (fix<G, Q>): the weights
-    of position p + 16 q are alpha^(-16 q e) times those of position p.  Encode evaluates the same
-    syndromes over the data positions (the kernel masks positions >= K) for k_ps_parity8."""
+    q, q + QN, q + 2 QN, ... and runs each piece's own networks on them (block index = the piece's
+    absolute 8-position block).  Encode evaluates the same syndromes over the data positions (the
+    kernel masks positions >= K) for k_ps_parity8."""
     out = []
     R = PtRole(c, False)
     st = f"PT_{c.name}"
@@ -552,8 +550,6 @@ def gen_pt(c: PsCodec):
            "    // positions 8B..8B+7 (words X) into group G's state (B: the absolute 8-position block;",
            "    // F: the wave's first block, which sets the state instead of accumulating into it)",
            "    template <int G, int B, bool F> static __device__ void block(uint32_t (&V)[NI][8], const uint32_t (&X)[8]);",
-           "    // group G's partials of quarter Q (computed with quarter 0's weights) times alpha^(-16 Q e)",
-           "    template <int G, int Q> static __device__ void fix(uint32_t (&V)[NI][8]);",
            "    template <int W, class F, class H> static __device__ void epilogue(const uint32_t (&T)[NOWN][8], F &&emit, "
            "H &&hook);",
            "};"]
@@ -562,23 +558,13 @@ def gen_pt(c: PsCodec):
     for g, gitems in enumerate(R.groups):
         ws = [R.wfun[i] for i in gitems]
         # every wave of group g runs its own pieces' networks (block index = absolute 8-position
-        # block), so no quarter needs a fix-up; fix<> stays for the shared-network variant
+        # block), so no quarter needs a fix-up
         pall = sorted(set(p for w in range(W) if R.waves[w]["g"] == g for p in R.pieces[w][0] + R.pieces[w][1]))
         for pc in pall:
             for B in (2 * pc, 2 * pc + 1):
                 for F in ((True, False) if B == 2 * pc else (False,)):
                     emit_weight_block(out, f"template <> __device__ __forceinline__ void {st}::block<{g}, {B}, {str(F).lower()}>("
                                       "uint32_t (&V)[NI][8], const uint32_t (&X)[8])", ws, B, first=F, opaque=True)
-        for q in range(1, R.qn):
-            out.append(f"template <> __device__ __forceinline__ void {st}::fix<{g}, {q}>(uint32_t (&V)[NI][8]) {{")
-            out.append("    uint32_t t[8];")
-            for s, i in enumerate(gitems):
-                e = c.exps[c.leaders[i]]
-                cst = gf.pow_alpha((-16 * q * e) % N)
-                rows = lin_rows(lambda x, cst=cst: gf.mul(cst, x))
-                out.append(f"    for (int b = 0; b < 8; ++b) t[b] = V[{s}][b];")
-                mat_apply(out, [f"V[{s}][{b}]" for b in range(8)], [f"t[{b}]" for b in range(8)], rows, "    ")
-            out.append("}")
     for w in range(W):
         emit_fold_epilogue(out, c.gf, f"{st}_epi{w}", "T", f"{st}::NOWN", R.waves[w]["seq"])
     out.append(f"template <int W, class F, class H> __device__ __forceinline__ void {st}::epilogue("

@@ -110,7 +110,7 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
     unsigned sv[32];
 #pragma unroll
     for (int i = 0; i < 32; ++i) sv[i] = syn_in && i < (int)NR ? syn_in[i * syn_step] : 0u;
-    const bool eras_vec = (reinterpret_cast<uintptr_t>(eras) & 15) == 0 && eras_cap >= 4;
+    const bool eras_vec = eras != nullptr && (reinterpret_cast<uintptr_t>(eras) & 15) == 0 && eras_cap >= 4;
     uint4 v[8];
     if (eras_vec) __builtin_memcpy(&v[0], eras, 16);
     if (len == 0 || len > LOAD) return -1;                                    // 1375-1377
@@ -390,13 +390,13 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
             // Karn applies den == 0 (log A0 = NN: the correction is num1 * num2) and skips a root
             // in the pad (decode_rs.h:277-289); ezpwd fails both (1625-1648)
             if (den == 0 && !karn) { count = -1; break; }
+            const unsigned loc = (rj * c.iprim + 254u) % 255u;
+            if (karn && loc < pad) {                  // skipped, as libfec does: no correction, and
+                if (corr_out) corr_out[j] = 0;        // corr 0 whatever the error value
+                continue;                             // (include/ezrs.h)
+            }
             if (num1 != 0) {
-                const unsigned loc = (rj * c.iprim + 254u) % 255u;
                 if (loc < pad) {
-                    if (karn) {                       // skipped, as libfec does: no correction
-                        if (corr_out) corr_out[j] = 0;
-                        continue;
-                    }
                     count = -1;
                     break;
                 }
@@ -549,7 +549,7 @@ __global__ void __launch_bounds__(64 * kWaves) k_decode_errors(DevCodec c, Decod
                 const bool synz = a.result[k] != kSentinel;
                 const bool tiled = layout == SynLayout::Tiled;
                 const uint8_t *syn = tiled ? syn_ws + k / 256 * kSynTile + k % 256 : syn_ws + k * 32;
-                const unsigned cap = a.eras_stride < 32 ? (unsigned)a.eras_stride : 32u;
+                const unsigned cap = !eras ? 0u : a.eras_stride < 32 ? (unsigned)a.eras_stride : 32u;
                 a.result[k] = decode_lane(c, L, W, lane, data, len, parity, eras, ne, cap, pos, corr,
                                           syn_ws ? syn : nullptr, tiled ? 256u : 1u, synz);
             }

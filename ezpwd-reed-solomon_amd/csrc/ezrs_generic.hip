@@ -369,12 +369,12 @@ __device__ int decode_one(const DevCodec &c, const uint16_t *__restrict__ A,
         // Karn applies den == 0 (its log is A0 = NN: the correction is num1 * num2) and skips a
         // root in the pad (decode_rs.h:277-289); ezpwd fails both (1625-1648)
         if (den == 0 && !karn) { count = -1; goto finish; }
+        if (karn && locof(j) < pad) {                 // skipped, as libfec does: no correction, and
+            if (corr_out) corr_out[j] = static_cast<T>(0);   // corr 0 whatever the error value
+            continue;                                 // (include/ezrs.h)
+        }
         if (num1 != 0) {
             if (locof(j) < pad) {
-                if (karn) {                           // skipped, as libfec does: no correction
-                    if (corr_out) corr_out[j] = static_cast<T>(0);
-                    continue;
-                }
                 count = -1;
                 goto finish;
             }

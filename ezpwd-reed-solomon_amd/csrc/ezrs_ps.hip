@@ -55,12 +55,6 @@ constexpr int kN = 255;
 
 typedef __attribute__((address_space(3))) void lds_void;
 
-#ifndef EZRS_PQ_MAINPRIO
-#define EZRS_PQ_MAINPRIO 1
-#endif
-#ifndef EZRS_PT_PRIO
-#define EZRS_PT_PRIO 3                // every main loop at s_setprio 1: r04k C2 on k_pt_lin 1115 vs 1091 GB/s
-#endif
 #ifdef EZRS_PS_STAMPS
 // tools/micro/pt_stamps.hip: phase stamps of the linear tile kernel, [wg][wave][tile][phase]
 __device__ unsigned long long g_pt_stamps[16][8][8][8];
@@ -207,19 +201,6 @@ __device__ __forceinline__ void barrier() { asm volatile("s_barrier" ::: "memory
 
 __device__ __forceinline__ void store_dword(pw_rsrc_t r, uint32_t off, uint32_t v) {
     asm volatile("buffer_store_dword %0, %1, %2, 0 offen" :: "v"(v), "v"(off), "s"(r) : "memory");
-}
-// A/B (EZRS_SYN_POLICY): the encode syndrome workspace stores with a cache policy -- 1 nt, 2 sc1,
-// 3 sc0 sc1 -- to see whether the dirty lines the next launch waits on set the gap between them
-__device__ __forceinline__ void store_dword_syn(pw_rsrc_t r, uint32_t off, uint32_t v) {
-#if defined(EZRS_SYN_POLICY) && EZRS_SYN_POLICY == 1
-    asm volatile("buffer_store_dword %0, %1, %2, 0 offen nt" :: "v"(v), "v"(off), "s"(r) : "memory");
-#elif defined(EZRS_SYN_POLICY) && EZRS_SYN_POLICY == 2
-    asm volatile("buffer_store_dword %0, %1, %2, 0 offen sc1" :: "v"(v), "v"(off), "s"(r) : "memory");
-#elif defined(EZRS_SYN_POLICY) && EZRS_SYN_POLICY == 3
-    asm volatile("buffer_store_dword %0, %1, %2, 0 offen sc0 sc1" :: "v"(v), "v"(off), "s"(r) : "memory");
-#else
-    store_dword(r, off, v);
-#endif
 }
 __device__ __forceinline__ void store_byte(pw_rsrc_t r, uint32_t off, uint32_t v) {
     asm volatile("buffer_store_byte %0, %1, %2, 0 offen" :: "v"(v), "v"(off), "s"(r) : "memory");
@@ -434,17 +415,11 @@ __device__ __forceinline__ void read_rows_shard(u32x4 (&R)[4], uint32_t lbuf, in
     }
 }
 
-// Quarter Q's pieces.  Default: each piece runs its own networks (block index = its absolute
-// 8-position block).  EZRS_PT_SHARED_NETS (variant builds): quarter 0's networks on every quarter,
-// then fix<G, Q> multiplies the partials by alpha^(-16 Q e) (smaller code, more VALU).
+// Quarter Q's pieces, each with its own networks (block index = its absolute 8-position block).
 template <class C, int G, int Q, int HI, bool SH, bool LO0>
 __device__ __forceinline__ void lin_pass(uint32_t (&V)[C::NI][8], uint32_t lbuf, uint32_t stride, int lo,
                                          const uint32_t (&ph)[4], int tail_lo) {
-#ifdef EZRS_PT_SHARED_NETS
-    constexpr int BQ = 0;
-#else
     constexpr int BQ = Q;
-#endif
     constexpr int NP = C::NP0[G] + C::NP1[G];
     static_assert(16 * (C::PIECE[G][0] + Q) < HI, "the wave's first block sets its state");
     u32x4 e = {0, 0, 0, 0};
@@ -488,9 +463,6 @@ __device__ __forceinline__ void wave_tail_lin(uint32_t (&V)[C::NI][8], const PsA
     (void)pt_it; (void)pt_w;
     constexpr int G = W % C::GN, Q = W / C::GN;
     if (!(a.ablate & 2)) {
-#ifdef EZRS_PT_SHARED_NETS
-        if constexpr (Q > 0) C::template fix<G, Q>(V);      // quarter 0's weights -> this quarter's
-#endif
         exchange<C, W, 0>(V, lbuf + 16u * fresh());         // slot (W XCAP + j) at 2 KiB each
     }
     PT_STAMP(4);
@@ -644,22 +616,15 @@ __device__ __forceinline__ void pt_run_lin(const PsArgs &a, uint8_t *lds) {
             }
             barrier();
         }
-#if EZRS_PT_PRIO
-        // main loop priority: 3 (default) = every wave over the other workgroup's tails; timing
-        // builds: 0 = none, 1 = waves 4..7 first, 2 = by quarter
-        if (EZRS_PT_PRIO == 1 && w >= 4) asm volatile("s_setprio 1");
-        if (EZRS_PT_PRIO == 2) { if (w >= 6) asm volatile("s_setprio 3"); else if (w >= 4) asm volatile("s_setprio 2"); else if (w >= 2) asm volatile("s_setprio 1"); }
-        if (EZRS_PT_PRIO == 3) asm volatile("s_setprio 1");  // every main loop over the tails
-#endif
+        // every main loop over the other workgroup's tails (r04k C2 on k_pt_lin 1115 vs 1091 GB/s)
+        asm volatile("s_setprio 1");
         int tlo = lo;                                        // shard batches: pad of the tile's rows
         if constexpr (SH) {
             const uint32_t t0 = tile * kTile, kt = (t0 / a.srows) * a.srows + a.srows - 1;
             if (kt < t0 + kTile && kt < a.ncw) tlo = a.stail_lo;
         }
         lin_pass<C, G, Q, HI, SH, LO0>(V, lbuf, a.stride, lo, ph, tlo);
-#if EZRS_PT_PRIO
         asm volatile("s_setprio 0");
-#endif
         PT_STAMP(2);
         barrier();                                           // the image is consumed
         PT_STAMP(3);
@@ -692,87 +657,6 @@ k_pt_lin(PsArgs a) {
 
 } // namespace pt
 
-namespace xpk {
-using pt::u32x4;
-constexpr int kXArea = 32768;                 // at most 16 items of 2 KiB per sub-round
-// Packed exchange (k_pq_lin, k_pq2): window [J0, J0 + 4) of sub-round S of the generated plan (XS / XV),
-// the items of all waves of the window packed one after the other (2 KiB each) in an area of at most
-// kXArea bytes; a window no wave uses is skipped.
-template <class C, int S, int J0, int W>
-constexpr int xbase() {
-    int n = 0;
-    for (int w = 0; w < W; ++w)
-        for (int j = J0; j < J0 + 4 && j < C::XCAP; ++j) n += C::XS[w][S][j] >= 0;
-    return n;
-}
-// index of item j among wave W's sent items of the window
-template <class C, int S, int J0, int W>
-constexpr int xidx(int j) {
-    int n = 0;
-    for (int i = J0; i < j; ++i) n += C::XS[W][S][i] >= 0;
-    return n;
-}
-template <class C, int S, int J0>
-constexpr int xtotal() {
-    int n = 0;
-    for (int w = 0; w < 4; ++w)
-        for (int j = J0; j < J0 + 4 && j < C::XCAP; ++j) n += C::XS[w][S][j] >= 0;
-    return n;
-}
-template <class C, int S, int J0, int W, int J = J0>
-__device__ __forceinline__ void xsend(uint32_t (&V)[C::NI][8], uint32_t lx) {
-    if constexpr (J < J0 + 4 && J < C::XCAP) {
-        constexpr int it = C::XS[W][S][J];
-        if constexpr (it >= 0) {
-            constexpr int slot = xbase<C, S, J0, W>() + xidx<C, S, J0, W>(J);
-            const u32x4 w0 = {V[it][0], V[it][1], V[it][2], V[it][3]};
-            const u32x4 w1 = {V[it][4], V[it][5], V[it][6], V[it][7]};
-            asm volatile("ds_write_b128 %0, %1 offset:%3\n\t"
-                         "ds_write_b128 %0, %2 offset:%4"
-                         :: "v"(lx), "v"(w0), "v"(w1), "n"(slot * 2048), "n"(slot * 2048 + 1024) : "memory");
-        }
-        xsend<C, S, J0, W, J + 1>(V, lx);
-    }
-}
-template <class C, int S, int J0, int W, int PW, int J = J0>
-__device__ __forceinline__ void xrecv(uint32_t (&V)[C::NI][8], uint32_t lx) {
-    if constexpr (J < J0 + 4 && J < C::XCAP) {
-        constexpr int it = C::XV[W][S][J];
-        if constexpr (it >= 0) {
-            static_assert(C::XS[PW][S][J] >= 0, "partner sends what this wave adds");
-            constexpr int slot = xbase<C, S, J0, PW>() + xidx<C, S, J0, PW>(J);
-            u32x4 b[2];
-            asm volatile("ds_read_b128 %0, %2 offset:%3\n\t"
-                         "ds_read_b128 %1, %2 offset:%4\n\t"
-                         "s_waitcnt lgkmcnt(0)"
-                         : "=&v"(b[0]), "=&v"(b[1]) : "v"(lx), "n"(slot * 2048), "n"(slot * 2048 + 1024) : "memory");
-            V[it][0] ^= b[0].x; V[it][1] ^= b[0].y; V[it][2] ^= b[0].z; V[it][3] ^= b[0].w;
-            V[it][4] ^= b[1].x; V[it][5] ^= b[1].y; V[it][6] ^= b[1].z; V[it][7] ^= b[1].w;
-        }
-        xrecv<C, S, J0, W, PW, J + 1>(V, lx);
-    }
-}
-template <class C, int W, int S = 0, int J0 = 0>
-__device__ __forceinline__ void exchange(uint32_t (&V)[C::NI][8], uint32_t lx) {
-    if constexpr (S < C::NSUB) {
-        if constexpr (J0 >= C::XCAP) {
-            exchange<C, W, S + 1, 0>(V, lx);
-        } else {
-            if constexpr (xtotal<C, S, J0>() > 0) {
-                static_assert(xtotal<C, S, J0>() * 2048 <= kXArea, "sub-round fits the area");
-                xsend<C, S, J0, W>(V, lx);
-                pt::wait_lgkm();
-                pt::barrier();
-                xrecv<C, S, J0, W, W ^ (1 << C::XR[S])>(V, lx);
-                pt::barrier();                               // read before the area is reused
-            }
-            exchange<C, W, S, J0 + 4>(V, lx);
-        }
-    }
-}
-
-} // namespace xpk
-
 // ---- 4-wave tile kernel k_pq_lin (PQ_<codec>, codegen gen_pq) -----------------------------------
 // One 256-thread workgroup (4 waves) per 256-codeword tile, two workgroups per CU (80 KiB LDS
 // each), up to 256 VGPRs (2 waves per SIMD).  Wave W evaluates EVERY coset leader (NI x 8 state
@@ -795,11 +679,6 @@ constexpr int kLds = 81920;                   // 80 KiB: two workgroups per CU
 constexpr int kFlags = kGuard + kImage;       // decode flags [4][64] after the image
 constexpr int kTab = kFlags + 1024;           // shard batches: per-row image offset and pad [256]
 static_assert(kTab + 1024 <= kLds, "pq tile kernel LDS");
-// the packed exchange's area at the top of the LDS (over the image's last 16 KiB and the flags and
-// row table, whose uses do not overlap the exchange); the DMA instructions below it (kEarly) go out
-// before the exchange
-constexpr int kXBase = kLds - xpk::kXArea;
-constexpr int kEarly = (kXBase - kGuard) / 1024;
 
 // Raw dwords of rows 4l + k at one 16-position piece (4-byte aligned reads, aligned afterwards).
 struct Raw {
@@ -920,9 +799,7 @@ __device__ __forceinline__ void piece(uint32_t (&V)[C::NI][8], Raw &cur, const u
     if constexpr (B < b1) {
         wait_raw(cur);
         Raw nxt;
-#ifndef EZRS_PQ_NOPREFETCH
         if constexpr (B + 2 < b1) issue_piece<8 * (B + 2), (B + 3 >= b1)>(nxt, at4);
-#endif
         __builtin_amdgcn_sched_barrier(0);
         u32x4 R[4];
         align_rows<SH>(R, cur, at, 8 * B, tail_lo, pads);
@@ -943,9 +820,6 @@ __device__ __forceinline__ void piece(uint32_t (&V)[C::NI][8], Raw &cur, const u
             block8<C, HI, B + 1, false, LO0>(V, X, lo);
         }
         __builtin_amdgcn_sched_barrier(0);
-#ifdef EZRS_PQ_NOPREFETCH
-        if constexpr (B + 2 < b1) issue_piece<8 * (B + 2), (B + 3 >= b1)>(nxt, at4);
-#endif
         if constexpr (B + 2 < b1) piece<C, ENC, W, SH, LO0, I + 1>(V, nxt, at, at4, lo, tail_lo, pads);
     }
 }
@@ -1003,66 +877,19 @@ __device__ __forceinline__ void exchange(uint32_t (&V)[C::NI][8], uint32_t lx) {
     }
 }
 
-// instructions [i0, i1) of the tile's DMA, wave w taking every fourth
-__device__ __forceinline__ void issue_tile(uint32_t lbuf, pw_rsrc_t rsrc, uint32_t toff, uint32_t tile_bytes, int w,
-                                           uint32_t i0 = 0, uint32_t i1 = 64) {
+// The tile's DMA, wave w taking every fourth 1 KiB instruction
+__device__ __forceinline__ void issue_tile(uint32_t lbuf, pw_rsrc_t rsrc, uint32_t toff, uint32_t tile_bytes, int w) {
 #ifdef EZRS_PQ_ABL_NODMA
     return;                                                  // timing-only builds (pq_stamps)
 #endif
-    const uint32_t ninstr = min((tile_bytes + 1023) >> 10, i1);
+    const uint32_t ninstr = (tile_bytes + 1023) >> 10;
     const uint32_t lo16 = 16u * pt::fresh();
-#ifdef EZRS_PQ_DMA_M0X4
-    // wave w: pieces 16w .. 16w+15, four per M0 value (the instruction offset steps both the
-    // source and the LDS destination)
-    for (uint32_t i = 16u * (uint32_t)w; i < 16u * (uint32_t)w + 16u && i < ninstr; i += 4) {
-        if (i + 4 <= ninstr)
-            asm volatile("s_mov_b32 m0, %0\n\t"
-                         "s_nop 0\n\t"
-                         "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
-                         "buffer_load_dwordx4 %1, %2, 0 offen offset:1024 lds\n\t"
-                         "buffer_load_dwordx4 %1, %2, 0 offen offset:2048 lds\n\t"
-                         "buffer_load_dwordx4 %1, %2, 0 offen offset:3072 lds"
-                         :: "s"(lbuf + kGuard + i * 1024u), "v"(toff + i * 1024u + lo16), "s"(rsrc) : "memory", "m0");
-        else
-            for (uint32_t j = i; j < ninstr; ++j)
-                asm volatile("s_mov_b32 m0, %0\n\t"
-                             "s_nop 0\n\t"
-                             "buffer_load_dwordx4 %1, %2, 0 offen lds"
-                             :: "s"(lbuf + kGuard + j * 1024u), "v"(toff + j * 1024u + lo16), "s"(rsrc) : "memory", "m0");
-    }
-#else
-    for (uint32_t i = i0 + (uint32_t)((w - (int)i0) & 3); i < ninstr; i += kWaves)
+    for (uint32_t i = (uint32_t)w; i < ninstr; i += kWaves)
         asm volatile("s_mov_b32 m0, %0\n\t"
                      "s_nop 0\n\t"
                      "buffer_load_dwordx4 %1, %2, 0 offen lds"
                      :: "s"(lbuf + kGuard + i * 1024u), "v"(toff + i * 1024u + lo16), "s"(rsrc) : "memory", "m0");
-#endif
 }
-
-#ifdef EZRS_PQ_DMA_SPREAD
-// Group g (0..3) of wave w's pieces 16w + 4g .. 16w + 4g + 3, four per M0 value (the instruction
-// offset steps both the source and the LDS destination), issued between fold steps.
-__device__ __forceinline__ void issue_group(uint32_t lbuf, pw_rsrc_t rsrc, uint32_t toff, uint32_t tile_bytes, int w,
-                                            int g) {
-    const uint32_t ninstr = (tile_bytes + 1023) >> 10;
-    const uint32_t lo16 = 16u * pt::fresh();
-    const uint32_t i = 16u * (uint32_t)w + 4u * (uint32_t)g;
-    if (i + 4 <= ninstr)
-        asm volatile("s_mov_b32 m0, %0\n\t"
-                     "s_nop 0\n\t"
-                     "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
-                     "buffer_load_dwordx4 %1, %2, 0 offen offset:1024 lds\n\t"
-                     "buffer_load_dwordx4 %1, %2, 0 offen offset:2048 lds\n\t"
-                     "buffer_load_dwordx4 %1, %2, 0 offen offset:3072 lds"
-                     :: "s"(lbuf + kGuard + i * 1024u), "v"(toff + i * 1024u + lo16), "s"(rsrc) : "memory", "m0");
-    else
-        for (uint32_t j = i; j < ninstr && j < i + 4; ++j)
-            asm volatile("s_mov_b32 m0, %0\n\t"
-                         "s_nop 0\n\t"
-                         "buffer_load_dwordx4 %1, %2, 0 offen lds"
-                         :: "s"(lbuf + kGuard + j * 1024u), "v"(toff + j * 1024u + lo16), "s"(rsrc) : "memory", "m0");
-}
-#endif
 
 // Exchange, next tile's DMA, fold and stores of wave W.
 template <class C, bool ENC, int W>
@@ -1070,29 +897,15 @@ __device__ __forceinline__ void wave_tail(uint32_t (&V)[C::NI][8], const PsArgs 
                                           uint32_t noff, uint32_t nbytes, pw_rsrc_t rsrc, pw_rsrc_t rout,
                                           pw_rsrc_t rws, int pq_it = 0) {
     (void)pq_it;
-#ifdef EZRS_PQ_EARLYDMA
-    // (measured and dropped, opt-in: decode 0.072 vs 0.066 ms) the next tile's first kEarly KiB land in the image below the exchange area as soon as the
-    // main loop has consumed it; the rest once the exchange (at the top of the LDS) is done
-    if (noff != kOob) issue_tile(lbuf, rsrc, noff, nbytes, W, 0, kEarly);
-    xpk::exchange<C, W>(V, lbuf + (uint32_t)kXBase + 16u * pt::fresh());
-    PQ_STAMP(4);
-    if (noff != kOob) issue_tile(lbuf, rsrc, noff, nbytes, W, kEarly, 64);
-#else
     exchange<C, W, 0>(V, lbuf + 16u * pt::fresh());
     PQ_STAMP(4);
-#if !defined(EZRS_PQ_DMA_LATE) && !defined(EZRS_PQ_DMA_SPREAD)
     if (noff != kOob) issue_tile(lbuf, rsrc, noff, nbytes, W);
-#endif
-#endif
     uint32_t T[C::NOWN][8];
 #pragma unroll
     for (int i = 0; i < C::NOWN; ++i)
 #pragma unroll
         for (int t = 0; t < 8; ++t) T[i][t] = C::OWN[W][i] >= 0 ? V[C::OWN[W][i] < 0 ? 0 : C::OWN[W][i]][t] : 0u;
     uint32_t Qs[C::NQ][8], nz = 0;
-#ifdef EZRS_PQ_FOLDPRIO
-    asm volatile("s_setprio %0" :: "n"(EZRS_PQ_FOLDPRIO));
-#endif
     C::template epilogue<W>(T, [&](auto qc, uint32_t (&Qw)[8]) {
         constexpr int qd = decltype(qc)::value;
         constexpr uint32_t vm = (C::SYN[W][qd][0] >= 0 ? 0x01010101u : 0u) | (C::SYN[W][qd][1] >= 0 ? 0x02020202u : 0u) |
@@ -1102,22 +915,8 @@ __device__ __forceinline__ void wave_tail(uint32_t (&V)[C::NI][8], const PsArgs 
             nz |= Qw[t] & vm;
             Qs[qd][t] = Qw[t];
         }
-    }, [&](auto pc) {
-#ifdef EZRS_PQ_DMA_SPREAD
-        constexpr int pt_ = decltype(pc)::value;             // DMA groups at fold points 1, 3, 5, 7
-        if constexpr (pt_ % 2 == 1 && pt_ < 8)
-            if (noff != kOob) issue_group(lbuf, rsrc, noff, nbytes, W, pt_ / 2);
-#else
-        (void)pc;
-#endif
-    });
+    }, [](auto) {});
     PQ_STAMP(5);
-#ifdef EZRS_PQ_FOLDPRIO
-    asm volatile("s_setprio 0");
-#endif
-#ifdef EZRS_PQ_DMA_LATE
-    if (noff != kOob) issue_tile(lbuf, rsrc, noff, nbytes, W);
-#endif
     const uint32_t cw0 = tile * kTile + 4u * pt::fresh();    // byte k <-> codeword cw0 + k
     if constexpr (ENC) {
         static_for<0, C::NQ>([&](auto qc) {
@@ -1126,7 +925,7 @@ __device__ __forceinline__ void wave_tail(uint32_t (&V)[C::NI][8], const PsArgs 
 #pragma unroll
             for (int jj = 0; jj < 4; ++jj)
                 if (C::SYN[W][qd][jj] >= 0)
-                    pt::store_dword_syn(rws, (uint32_t)(C::SYN[W][qd][jj] * a.ws_pitch) + cw0, Qs[qd][jj]);
+                    pt::store_dword(rws, (uint32_t)(C::SYN[W][qd][jj] * a.ws_pitch) + cw0, Qs[qd][jj]);
         });
     } else {
         uint32_t fl = 0;
@@ -1239,15 +1038,12 @@ __device__ __forceinline__ void pq_run(const PsArgs &a, uint8_t *lds) {
             if (kt < t0 + kTile && kt < a.ncw) tlo = a.stail_lo;
         }
         PQ_STAMP(1);
-#ifndef EZRS_PQ_NOPRIO
         // the main loop outranks the other workgroup's waves on the SIMD (their exchange, DMA and
-        // fold): r04j C2 1203 vs 1169 GB/s
-        asm volatile("s_setprio %0" :: "n"(EZRS_PQ_MAINPRIO));
-#endif
+        // fold): r04j C2 1203 vs 1169 GB/s; r06c: tails over main loops 1503, equal priority 1430,
+        // main loops over tails 1558 GB/s (profiles/r06/r06c_priority_ab.txt)
+        asm volatile("s_setprio 1");
         pq_pass<C, ENC, W, SH, LO0>(V, lbuf, a.stride, lo, tlo);
-#ifndef EZRS_PQ_NOPRIO
         asm volatile("s_setprio 0");
-#endif
         PQ_STAMP(2);
         pt::barrier();                                       // the image is consumed
         PQ_STAMP(3);
@@ -1276,318 +1072,6 @@ k_pq_lin(PsArgs a) {
 
 } // namespace pq
 
-// ---- double-buffered 4-wave tile kernel k_pq2 (PQ_<codec> networks, full-length packed rows) ------
-// The tile's 256 rows are taken in two position chunks, 0..127 and 128..254, each with its own 36 KiB
-// LDS slot: the next tile's chunk 0 is DMA'd into slot 0 while this tile's chunk 1 is processed (its
-// issues spread through that main loop), and its chunk 1 into slot 1 once this tile's exchange has
-// released the slot (spread through the fold).  k_pq_lin has one 64 KiB image per workgroup, so its
-// next tile's DMA could only start after the exchange; r05d stamps on clean data: of 17.0 k ticks
-// per tile, 5.4 k were the wave waiting for that DMA.
-//   * A chunk slot holds 9 aligned 16-byte pieces per row (a row's chunk spans at most 143 bytes
-//     with its 16-byte phase): the pieces are gathered by LDS-DMA with per-lane source addresses;
-//     every instruction's 1 KiB covers whole rows' pieces (about 7 rows), so a line is fetched
-//     once per chunk.
-//   * Row r's pieces sit at slot position sigma(r) = (l >> 2) + 16 (l & 3) + 64 k for r = 4 l + k:
-//     lane l reads its rows 4l + k (the codeword mapping of k_pq_lin, so every workspace layout is
-//     unchanged) at dword addresses 36 sigma + phase / 4, which fall in 32 distinct banks per half
-//     wave for each k.
-//   * The exchange runs in slot 1 in sub-rounds of at most 32 KiB (items packed over the waves).
-// Used for plain batches of full-length RS(255,223) rows at pitch 255 with a 16-byte aligned base;
-// every other geometry keeps k_pq_lin.
-namespace pq2 {
-
-using pt::kOob;
-using pt::u32x2;
-using pt::u32x4;
-using pq::Raw;
-constexpr int kThreads = 256;
-constexpr int kWaves = 4;
-constexpr int kPitch = 144;                   // bytes per row in a chunk slot: 9 pieces
-constexpr int kSlot = 256 * kPitch;           // 36 KiB = 36 DMA instructions of 1 KiB
-constexpr int kInstrW = kSlot / 1024 / kWaves;    // 9 per wave per chunk
-constexpr int kFlags = 2 * kSlot;             // decode flags [4][64]
-constexpr int kLds = kFlags + 1024;
-static_assert(kLds <= 81920, "two workgroups per CU");
-static_assert(kSlot % (1024 * kWaves) == 0, "whole DMA instructions per wave");
-
-__host__ __device__ constexpr uint32_t slot_pos(uint32_t r) {
-    return ((r >> 2) >> 2) + 16u * ((r >> 2) & 3u) + 64u * (r & 3u);
-}
-__host__ __device__ constexpr uint32_t row_of(uint32_t sig) {
-    return 4u * (4u * (sig & 15u) + ((sig & 63u) >> 4)) + (sig >> 6);
-}
-static_assert(row_of(slot_pos(137)) == 137 && row_of(slot_pos(255)) == 255 && row_of(slot_pos(4)) == 4, "slot map");
-
-// wave W's DMA source offsets (from the tile's first byte) for its pieces n = 0..8 of a chunk:
-// instruction j = W + 4n, lane i -> slot piece s = 64 j + i -> row row_of(s / 9), piece s % 9
-template <int W>
-__device__ __forceinline__ void dma_offsets(uint32_t (&off)[kInstrW]) {
-    const uint32_t lane = pt::fresh();
-#pragma unroll
-    for (int n = 0; n < kInstrW; ++n) {
-        const uint32_t s = 64u * (uint32_t)(W + 4 * n) + lane, sig = s / 9u, pc = s - 9u * sig;
-        off[n] = ((255u * row_of(sig)) & ~15u) + 16u * pc;
-    }
-}
-__device__ __forceinline__ void dma_piece(uint32_t m0, uint32_t voff, pw_rsrc_t rsrc) {
-    asm volatile("s_mov_b32 m0, %0\n\t"
-                 "s_nop 0\n\t"
-                 "buffer_load_dwordx4 %1, %2, 0 offen lds"
-                 :: "s"(m0), "v"(voff), "s"(rsrc) : "memory", "m0");
-}
-// wave W's pieces N0 .. N1-1 of chunk c of the tile whose first byte is at buffer offset tb
-template <int W, int N0, int N1>
-__device__ __forceinline__ void dma_run(const uint32_t (&off)[kInstrW], uint32_t lslot, uint32_t tb, pw_rsrc_t rsrc) {
-#pragma unroll
-    for (int n = N0; n < N1 && n < kInstrW; ++n) dma_piece(lslot + 1024u * (uint32_t)(W + 4 * n), off[n] + tb, rsrc);
-}
-
-// lane l's row k: dword-aligned LDS address of its chunk's position 0 (at4) and the byte phase
-// (at & 3, the v_alignbyte shift)
-__device__ __forceinline__ void row_addrs(uint32_t (&at)[4], uint32_t (&at4)[4], uint32_t lslot) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t r = 4u * pt::fresh() + k, ph = (0u - r) & 15u;   // (255 r) mod 16
-        at[k] = lslot + (uint32_t)kPitch * slot_pos(r) + ph;
-        at4[k] = at[k] & ~3u;
-    }
-}
-
-// Piece I of a run: blocks B, B+1 (absolute; positions from chunk c's first at OFF = 8 B - 128 c),
-// the next piece's reads in flight.  H(b) runs after block b (DMA issues).
-template <class C, int HI, int CH, int B, int B1, bool F, class H>
-__device__ __forceinline__ void piece(uint32_t (&V)[C::NI][8], Raw &cur, const uint32_t (&at)[4],
-                                      const uint32_t (&at4)[4], H &&hook) {
-    if constexpr (B < B1) {
-        pq::wait_raw(cur);
-        Raw nxt;
-        if constexpr (B + 2 < B1) pq::issue_piece<8 * (B + 2) - 128 * CH, (B + 3 >= B1)>(nxt, at4);
-        __builtin_amdgcn_sched_barrier(0);
-        u32x4 R[4];
-        pq::align_rows<false>(R, cur, at, 8 * B, 0, 0u);
-        uint32_t X[8];
-        {
-            const uint32_t c0[4] = {R[0].x, R[1].x, R[2].x, R[3].x};
-            const uint32_t c1[4] = {R[0].y, R[1].y, R[2].y, R[3].y};
-            transpose4x4(c0, X);
-            transpose4x4(c1, X + 4);
-        }
-        pq::block8<C, HI, B, F, true>(V, X, 0);
-        hook(std::integral_constant<int, B>{});
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (B + 1 < B1) {
-            const uint32_t c2[4] = {R[0].z, R[1].z, R[2].z, R[3].z};
-            const uint32_t c3[4] = {R[0].w, R[1].w, R[2].w, R[3].w};
-            transpose4x4(c2, X);
-            transpose4x4(c3, X + 4);
-            pq::block8<C, HI, B + 1, false, true>(V, X, 0);
-            hook(std::integral_constant<int, B + 1>{});
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (B + 2 < B1) piece<C, HI, CH, B + 2, B1, false, H>(V, nxt, at, at4, hook);
-    }
-}
-template <class C, int HI, int CH, int B0, int B1, bool F, class H>
-__device__ __forceinline__ void run(uint32_t (&V)[C::NI][8], uint32_t lslot, H &&hook) {
-    if constexpr (B0 < B1) {
-        uint32_t at[4], at4[4];
-        row_addrs(at, at4, lslot);
-        Raw cur;
-        pq::issue_piece<8 * B0 - 128 * CH, (B0 + 1 >= B1)>(cur, at4);
-        piece<C, HI, CH, B0, B1, F>(V, cur, at, at4, hook);
-    }
-}
-
-// wave W's blocks in chunk CH: decode 4 per wave per chunk (chunk 1's last block masks position
-// 255); encode chunk 1 holds the data blocks 16 .. 27, 3 per wave
-template <bool ENC, int W, int CH>
-struct Blocks {
-    static constexpr int PER = CH == 0 ? 4 : (ENC ? 3 : 4);
-    static constexpr int B0 = 16 * CH + PER * W, B1 = B0 + PER;
-};
-
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");
-}
-
-template <class C, bool ENC, int W>
-__device__ __forceinline__ void wave_run(const PsArgs &a, uint8_t *lds) {
-    constexpr int HI = ENC ? kN - (int)C::NR : kN;
-    constexpr uint32_t kTileBytes = 256u * 255u;
-    const pw_rsrc_t rsrc = pw_rsrc(a.base, a.span);
-    const uint32_t lbuf = __builtin_amdgcn_readfirstlane(lds_addr(lds));
-    const uint32_t ls0 = lbuf, ls1 = lbuf + (uint32_t)kSlot;
-    const pw_rsrc_t rout = pw_rsrc(reinterpret_cast<const uint8_t *>(a.result), ENC ? 0u : a.ncw * 4u);
-    const pw_rsrc_t rws = pw_rsrc(a.ws, ENC ? (uint32_t)(C::NR * a.ws_pitch) : (uint32_t)((a.ncw + 255) / 256 * kSynTile));
-    uint32_t off[kInstrW];
-    dma_offsets<W>(off);
-    uint32_t tile = blockIdx.x;
-    if (tile < a.ntiles) {
-        const uint32_t tb = tile * kTileBytes;
-        dma_run<W, 0, kInstrW>(off, ls0, tb, rsrc);
-        dma_run<W, 0, kInstrW>(off, ls1, tb + 128u, rsrc);
-    }
-    // stores this wave issued after the previous tile's chunk-1 DMAs (encode: fixed; decode: the
-    // results of wave 0 and, when the tile had a flagged codeword, the syndromes)
-    constexpr int NSYN = [] {
-        int n = 0;
-        for (int q = 0; q < C::NQ; ++q)
-            for (int j = 0; j < 4; ++j) n += C::SYN[W][q][j] >= 0;
-        return n;
-    }();
-    constexpr int NS0 = ENC ? NSYN : (W == 0 ? 4 : 0);
-    bool prev_flagged = false, first = true;
-    int pq_it = 0;
-    (void)pq_it;
-    PQ_RT(0);
-    for (; tile < a.ntiles; tile += gridDim.x, ++pq_it) {
-        PQ_STAMP(0);
-        const uint32_t next = tile + gridDim.x;
-        const bool has_next = next < a.ntiles;               // wave-uniform
-        const uint32_t tbn = next * kTileBytes;
-        uint32_t V[C::NI][8];                                // set by the wave's first block
-        // chunk 0 of this tile: every VMEM op but this wave's chunk-1 pieces and the stores after
-        // them has completed
-        if (first) wait_vm<kInstrW>();
-        else if (!ENC && prev_flagged) wait_vm<kInstrW + NS0 + NSYN>();
-        else wait_vm<kInstrW + NS0>();
-        pt::barrier();
-        PQ_STAMP(1);
-        asm volatile("s_setprio 1");
-        run<C, HI, 0, Blocks<ENC, W, 0>::B0, Blocks<ENC, W, 0>::B1, true>(V, ls0, [](auto) {});
-        asm volatile("s_setprio 0");
-        PQ_STAMP(2);
-        if (first) wait_vm<0>();                             // chunk 1 landed
-        else if (!ENC && prev_flagged) wait_vm<NS0 + NSYN>();
-        else wait_vm<NS0>();
-        first = false;
-        if (tile * kTileBytes + kTileBytes >= a.span && (a.span & 15u) != 0 && W == 0) {
-            // the last tile: a 16-byte piece that crosses the span's end came back all-zero; re-read
-            // its bytes inside the span one by one (out-of-range bytes read as zero) into the piece
-            const uint32_t pend = a.span & ~15u;             // the crossing piece's first byte
-            const uint32_t g = pend + pt::fresh();           // tile-relative offsets below
-            uint32_t v = 0;
-            if (pt::fresh() < 16u)
-                asm volatile("buffer_load_ubyte %0, %1, %2, 0 offen\n\ts_waitcnt vmcnt(0)"
-                             : "=&v"(v) : "v"(g), "s"(rsrc) : "memory");
-            const uint32_t t = g - tile * kTileBytes;         // the last row's chunk 1
-            const uint32_t r = (a.span - 1u - tile * kTileBytes) / 255u;
-            const uint32_t c1 = ((255u * r) & ~15u) + 128u; // its chunk-1 first piece
-            if (pt::fresh() < 16u && g < a.span && t >= c1 && t < c1 + (uint32_t)kPitch)
-                asm volatile("ds_write_b8 %0, %1\n\ts_waitcnt lgkmcnt(0)"
-                             :: "v"(ls1 + (uint32_t)kPitch * slot_pos(r) + (t - c1)), "v"(v) : "memory");
-        }
-        pt::barrier();                                       // chunk 1 visible; slot 0 consumed
-        PQ_STAMP(3);
-        asm volatile("s_setprio 1");
-        {
-            using BB = Blocks<ENC, W, 1>;
-            constexpr int NB = BB::B1 - BB::B0;
-            // the next tile's chunk 0 into slot 0, spread over this wave's chunk-1 blocks
-            run<C, HI, 1, BB::B0, BB::B1, false>(V, ls1, [&](auto bc) {
-                constexpr int i = decltype(bc)::value - BB::B0;
-                if (has_next) dma_run<W, (kInstrW * i + NB - 1) / NB, (kInstrW * (i + 1) + NB - 1) / NB>(off, ls0, tbn, rsrc);
-            });
-        }
-        asm volatile("s_setprio 0");
-        PQ_STAMP(4);
-        pt::barrier();                                       // slot 1 consumed
-        PQ_STAMP(5);
-        xpk::exchange<C, W>(V, ls1 + 16u * pt::fresh());
-        PQ_STAMP(6);
-        uint32_t T[C::NOWN][8];
-#pragma unroll
-        for (int i = 0; i < C::NOWN; ++i)
-#pragma unroll
-            for (int t = 0; t < 8; ++t) T[i][t] = C::OWN[W][i] >= 0 ? V[C::OWN[W][i] < 0 ? 0 : C::OWN[W][i]][t] : 0u;
-        uint32_t Qs[C::NQ][8], nz = 0;
-        C::template epilogue<W>(T, [&](auto qc, uint32_t (&Qw)[8]) {
-            constexpr int qd = decltype(qc)::value;
-            constexpr uint32_t vm = (C::SYN[W][qd][0] >= 0 ? 0x01010101u : 0u) | (C::SYN[W][qd][1] >= 0 ? 0x02020202u : 0u) |
-                                    (C::SYN[W][qd][2] >= 0 ? 0x04040404u : 0u) | (C::SYN[W][qd][3] >= 0 ? 0x08080808u : 0u);
-#pragma unroll
-            for (int t = 0; t < 8; ++t) {
-                nz |= Qw[t] & vm;
-                Qs[qd][t] = Qw[t];
-            }
-        }, [&](auto pc) {
-            // the next tile's chunk 1 into slot 1 (released by the exchange), over the fold
-            constexpr int h = decltype(pc)::value;
-            if (has_next) {
-                if constexpr (h == 0) dma_run<W, 0, 2>(off, ls1, tbn + 128u, rsrc);
-                else dma_run<W, h + 1, h + 2>(off, ls1, tbn + 128u, rsrc);
-            }
-        });
-        if (has_next) dma_run<W, 4 * C::NQ + 1, kInstrW>(off, ls1, tbn + 128u, rsrc);   // (fewer hooks)
-        PQ_STAMP(7);
-        const uint32_t cw0 = tile * 256u + 4u * pt::fresh();  // byte k <-> codeword cw0 + k
-        if constexpr (ENC) {
-            static_for<0, C::NQ>([&](auto qc) {
-                constexpr int qd = decltype(qc)::value;
-                transpose8(Qs[qd]);                          // Qs[qd][jj] byte k: syndrome jj, codeword k
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj)
-                    if (C::SYN[W][qd][jj] >= 0)
-                        pt::store_dword_syn(rws, (uint32_t)(C::SYN[W][qd][jj] * a.ws_pitch) + cw0, Qs[qd][jj]);
-            });
-        } else {
-            uint32_t fl = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (nz >> (8 * k) & 0xFF) fl |= 1u << k;
-            const uint32_t fa = lbuf + kFlags + 256u * W + 4u * pt::fresh();
-            asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" :: "v"(fa), "v"(fl) : "memory");
-            pt::barrier();
-            {
-                uint32_t f[4];
-                const uint32_t fb = lbuf + kFlags + 4u * pt::fresh();
-                asm volatile("ds_read_b32 %0, %4\n\t"
-                             "ds_read_b32 %1, %4 offset:256\n\t"
-                             "ds_read_b32 %2, %4 offset:512\n\t"
-                             "ds_read_b32 %3, %4 offset:768\n\t"
-                             "s_waitcnt lgkmcnt(0)"
-                             : "=&v"(f[0]), "=&v"(f[1]), "=&v"(f[2]), "=&v"(f[3]) : "v"(fb) : "memory");
-                fl = f[0] | f[1] | f[2] | f[3];
-            }
-            if constexpr (W == 0) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    pt::store_dword(rout, (cw0 + k) * 4u, (fl >> k & 1) ? (uint32_t)kSentinel : 0u);
-                if (fl != 0 && a.flag) *a.flag = a.gen;      // this call flagged a codeword
-            }
-            prev_flagged = __ballot(fl != 0) != 0;           // wave-uniform (the same for all waves)
-            if (prev_flagged) {                              // flagged codewords: their syndromes
-                static_for<0, C::NQ>([&](auto qc) {
-                    constexpr int qd = decltype(qc)::value;
-                    transpose8(Qs[qd]);
-#pragma unroll
-                    for (int jj = 0; jj < 4; ++jj)
-                        if (C::SYN[W][qd][jj] >= 0)
-                            pt::store_dword(rws, tile * (uint32_t)kSynTile + 256u * C::SYN[W][qd][jj] + 4u * pt::fresh(),
-                                            Qs[qd][jj]);
-                });
-            }
-        }
-    }
-    wait_vm<0>();                                            // no DMA may land after the exit
-    PQ_RT(1);
-}
-
-template <class C, bool ENC>
-__global__ void __attribute__((amdgpu_flat_work_group_size(kThreads, kThreads), amdgpu_waves_per_eu(2)))
-k_pq2(PsArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kLds];
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    switch (w) {
-    case 0: wave_run<C, ENC, 0>(a, lds); break;
-    case 1: wave_run<C, ENC, 1>(a, lds); break;
-    case 2: wave_run<C, ENC, 2>(a, lds); break;
-    default: wave_run<C, ENC, 3>(a, lds); break;
-    }
-}
-
-} // namespace pq2
 
 // ---- encode, stage 2: parity = V^-1 S on 32-codeword bit-sliced registers -------------------
 // Syndromes (encode workspace) -> parity rows.
@@ -1636,112 +1120,6 @@ __device__ __forceinline__ void store_parity_row(uint8_t *dst, const uint8_t *s8
     }
 }
 
-#ifdef EZRS_PAR_PIPE
-// Persistent, software-pipelined form of k_ps_parity8 (one 8-wave block per CU: planes and stage
-// in separate LDS, 130 KiB): chunk j's map runs while chunk j-1's parity rows drain to memory
-// (one quarter of the stores at each of four points of the pass) and chunk j+1's syndromes load
-// (issued once chunk j's last planes are written).  In k_ps_parity8 every block maps, then
-// stores, in lockstep with all the others (r04l stamps: map 10.8 us, stores 4-10 us, serial).
-template <class C>
-__global__ void __launch_bounds__(512) k_ps_parity_pipe(const uint8_t *ws, size_t ws_pitch, uint8_t *parity,
-                                                        size_t pstride, size_t ncw, Shards sh, unsigned len,
-                                                        unsigned nchunk) {
-    constexpr int NR = C::NR;
-    constexpr int kRegion = 32 * NR + 8;
-    constexpr int kPlanes = 8 * NR * kParGroups;               // dwords
-    constexpr int kStage = kParGroups * kRegion / 4;           // dwords
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kPlanes + kStage];
-    uint8_t *stage = reinterpret_cast<uint8_t *>(lds + kPlanes);
-    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    constexpr int NCH = (NR + 7) / 8;
-    constexpr int IL = 8 * (NCH - 1);                          // hooks 1 .. IL spread chunk j-1's stores
-    pt::u32x4 v[NCH][2];
-    auto load = [&](unsigned chunk) {
-        const uint8_t *src = ws + ((size_t)chunk * kParGroups + lane) * 32;
-#pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-            const int i = wave + 8 * c < NR ? wave + 8 * c : 0;
-            v[c][0] = *reinterpret_cast<const pt::u32x4 *>(src + i * ws_pitch);
-            v[c][1] = *reinterpret_cast<const pt::u32x4 *>(src + i * ws_pitch + 16);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    };
-    // every chunk's planes at once: a store in flight makes the compiler drain vmcnt to 0 at the
-    // next wait on a load (stores may complete out of order), so the planes are all in LDS before
-    // the pass interleaves the stores
-    auto ready_all = [&]() {
-        static_for<0, NCH>([&](auto cc) {
-            constexpr int c = decltype(cc)::value;
-            const int i = wave + 8 * c;
-            const pt::u32x4 a0 = v[c][0], a1 = v[c][1];
-            if (i < NR) {
-                uint32_t D[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-                transpose8(D);
-#pragma unroll
-                for (int qq = 0; qq < 8; ++qq) lds[(8 * i + qq) * 64 + lane] = D[qq];
-            }
-        });
-        pt::wait_lgkm();
-        pt::barrier();
-    };
-    auto store_part = [&](unsigned chunk, int j) {             // rows 512 j .. 512 j + 511 of a chunk
-        const int r = threadIdx.x + 512 * j;
-        const size_t k = (size_t)chunk * kParCw + r;
-        if (k < ncw) {
-            unsigned rlen;
-            uint8_t *dst = sh.rows ? parity + shard_row(sh, k, pstride, len, rlen) + rlen : parity + k * pstride;
-            store_parity_row<NR>(dst, stage + (r >> 5) * kRegion + (r & 31) * NR);
-        }
-    };
-    unsigned chunk = blockIdx.x, prev = 0xFFFFFFFFu;
-    if (chunk < nchunk) load(chunk);
-    for (; chunk < nchunk; chunk += gridDim.x) {
-        const unsigned next = chunk + gridDim.x;
-        ready_all();
-        auto hook = [&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            // chunk j-1's rows, a quarter at each of four points of the pass
-            static_for<0, 4>([&](auto jc) {
-                constexpr int jj = decltype(jc)::value;
-                if constexpr (IL > 0 && i == (jj + 1) * IL / 5)
-                    if (prev != 0xFFFFFFFFu) store_part(prev, jj);
-            });
-        };
-        uint32_t O[4][8];
-        pass_switch<C>(wave, O, lds + lane, hook);
-        if (wave >= C::NPASS4) static_for<1, NR>([&](auto ic) { hook(ic); });
-        if constexpr (IL == 0)                                 // no hook points: after the pass
-            if (prev != 0xFFFFFFFFu)
-                for (int j = 0; j < 4; ++j) store_part(prev, j);
-        pt::wait_lgkm();                                       // planes consumed, chunk j-1's stage read
-        pt::barrier();                                         // (raw barriers: loads stay in flight)
-        if (next < nchunk) load(next);                         // in flight through the stage phase
-        if (wave < C::NPASS4) {
-            const int nj = NR - 4 * wave < 4 ? NR - 4 * wave : 4;
-#pragma unroll
-            for (int jl = 0; jl < 4; ++jl)
-                if (jl < nj) transpose8(O[jl]);
-            uint8_t *reg = stage + lane * kRegion + 4 * wave;
-#pragma unroll
-            for (int m = 0; m < 8; ++m)
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    uint8_t *row = reg + (4 * m + k) * NR;
-                    if (nj == 4) {
-                        *reinterpret_cast<uint32_t *>(row) = gather4(O[0][m], O[1][m], O[2][m], O[3][m], k);
-                    } else {
-                        for (int jl = 0; jl < nj; ++jl) row[jl] = (uint8_t)(O[jl][m] >> (8 * k));
-                    }
-                }
-        }
-        pt::wait_lgkm();                                       // stage complete
-        pt::barrier();
-        prev = chunk;
-    }
-    if (prev != 0xFFFFFFFFu)
-        for (int j = 0; j < 4; ++j) store_part(prev, j);
-}
-#endif // EZRS_PAR_PIPE
 
 // 8-wave form of k_ps_parity: wave P computes parity symbols 4P..4P+3 (q_pass4), halving each
 // wave's share of the map and doubling the waves that hide the phases' latencies.
@@ -1769,27 +1147,6 @@ __global__ void __launch_bounds__(512) k_ps_parity8(const uint8_t *ws, size_t ws
         v[c][1] = *reinterpret_cast<const pt::u32x4 *>(src + i * ws_pitch + 16);
         __builtin_amdgcn_sched_barrier(0);                     // issue order = chunk order
     }
-#ifdef EZRS_PAR_NOCHUNK
-    auto ready = [&](auto cc) {                                // A/B: every chunk before the passes
-        if constexpr (decltype(cc)::value == 0) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            static_for<0, NCH>([&](auto c2) {
-                constexpr int c = decltype(c2)::value;
-                pt::u32x4 a0 = v[c][0], a1 = v[c][1];
-                asm volatile("" : "+v"(a0), "+v"(a1));
-                const int i = wave + 8 * c;
-                if (i < NR) {
-                    uint32_t D[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-                    transpose8(D);
-#pragma unroll
-                    for (int qq = 0; qq < 8; ++qq) lds[(8 * i + qq) * 64 + lane] = D[qq];
-                }
-            });
-            pt::wait_lgkm();
-            pt::barrier();
-        }
-    };
-#else
     auto ready = [&](auto cc) {
         constexpr int c = decltype(cc)::value;
         const int i = wave + 8 * c;
@@ -1803,7 +1160,6 @@ __global__ void __launch_bounds__(512) k_ps_parity8(const uint8_t *ws, size_t ws
         pt::wait_lgkm();                                       // raw barrier: later chunks' loads stay in flight
         pt::barrier();
     };
-#endif
     ready(std::integral_constant<int, 0>{});
     PAR_STAMP(1);
     PAR_STAMP(2);
@@ -1844,11 +1200,8 @@ __global__ void __launch_bounds__(512) k_ps_parity8(const uint8_t *ws, size_t ws
     // two lanes per parity row, NR / 2 bytes each (NR % 8 == 0): a wave's store covers 32 rows
     // instead of 64 (C2 line 1549 vs 1526 GB/s; 4 or 8 lanes per row the same within noise,
     // r05y / r05z A/B); other NR: one lane per row
-#ifndef EZRS_PAR_LPR
-#define EZRS_PAR_LPR 2
-#endif
-    if constexpr (NR % (4 * EZRS_PAR_LPR) == 0) {
-        constexpr int LPR = EZRS_PAR_LPR, PB = NR / LPR;
+    if constexpr (NR % 8 == 0) {
+        constexpr int LPR = 2, PB = NR / LPR;
         const int sub = threadIdx.x % LPR;
         for (int r = threadIdx.x / LPR; r < kParCw; r += 512 / LPR) {
             const size_t k = cwb + r;
@@ -1897,21 +1250,16 @@ template <class C> bool ps_matches(const DevCodec &d) {
            d.poly == C::POLY;
 }
 
-// The parity stage: k_ps_parity8, one block per chunk (default), or the pipelined persistent
-// kernel, one block per CU over the chunks (-DEZRS_PAR_PIPE, A/B builds: r04n 44.2 vs 41.2 us --
-// at two waves per SIMD the map loses more than the overlapped stores save).
+// The parity stage: k_ps_parity8, one block per 2048-codeword chunk.  Measured and dropped: a
+// pipelined persistent form, one block per CU over the chunks (r04n 44.2 vs 41.2 us: at two waves
+// per SIMD the map loses more than the overlapped stores save); independent waves without LDS,
+// each loading and transposing every syndrome itself (r06b 58 vs 38 us: four 8-byte partial
+// writes per row cost more than the whole LDS-staged kernel).
 template <class PS>
 void launch_parity(const DevCodec &d, const uint8_t *ws, size_t ws_pitch, uint8_t *par, size_t pstride,
                    size_t n, const Shards &sh, unsigned len, unsigned nchunk, hipStream_t s) {
-#ifndef EZRS_PAR_PIPE
     (void)d;
     hipLaunchKernelGGL((ps::k_ps_parity8<PS>), dim3(nchunk), dim3(512), 0, s, ws, ws_pitch, par, pstride, n, sh, len);
-#else
-    const unsigned ncu = d.ncu > 0 ? (unsigned)d.ncu : 256u;
-    const unsigned g = nchunk < ncu ? nchunk : ncu;
-    hipLaunchKernelGGL((ps::k_ps_parity_pipe<PS>), dim3(g), dim3(512), 0, s, ws, ws_pitch, par, pstride, n, sh, len,
-                       nchunk);
-#endif
 }
 
 // Workgroups per launch (persistent over tiles): 2 per CU (80 KiB LDS each).
@@ -1937,16 +1285,6 @@ void launch_tile(const ps::PsArgs &p, bool shard, unsigned grid, hipStream_t s) 
 #ifndef EZRS_NO_PQ
     if constexpr (!std::is_void<PQ>::value) {
         const bool lo0 = p.lo == 0;                          // full-length rows: no pad masks
-#ifdef EZRS_PQ2
-        // timing builds: plain batches of full-length packed rows from a 16-byte aligned base, each
-        // launch starting a tile of the syndrome layout, on the double-buffered kernel (r05e: C2
-        // 1381 vs 1450 GB/s -- its gathered DMA and the extra barriers cost more than the overlap
-        // gains; the early partial DMA of k_pq_lin is the default)
-        if (!shard && lo0 && p.stride == 255 && ((uintptr_t)p.base & 15) == 0 && (ENC || p.ws_pitch == 0)) {
-            hipLaunchKernelGGL((ps::pq2::k_pq2<PQ, ENC>), dim3(grid), dim3(ps::pq2::kThreads), 0, s, p);
-            return;
-        }
-#endif
         if (shard && lo0)
             hipLaunchKernelGGL((ps::pq::k_pq_lin<PQ, ENC, true, true>), dim3(grid), dim3(ps::pq::kThreads), 0, s, p);
         else if (shard)

@@ -28,8 +28,13 @@ CXXF      := -std=c++17 -O2 -w -I$(ROOT)/include -I$(REFERENCE)/c++ -I$(REFERENC
 TGZ       := $(REFERENCE)/phil-karn/fec-3.0.1.tar.gz
 KEX       := $(REFERENCE)/phil-karn/exercise.c
 
-.PHONY: all
+.PHONY: all FORCE
 all: $(OUT)/rsexercise $(OUT)/.karn_stamp
+FORCE:
+
+# the stamp stands for three binaries: if any of them is gone (a partial clean of _bin), rebuild
+KARN_BINS    := $(OUT)/rsvalidate $(OUT)/rsspeed $(OUT)/rstest
+KARN_MISSING := $(filter-out $(wildcard $(KARN_BINS)),$(KARN_BINS))
 
 $(OUT)/rsexercise: $(REFERENCE)/rsexercise.C $(REFERENCE)/exercise.H $(ROOT)/include/ezpwd_amd/rs
 	@mkdir -p $(OUT)
@@ -38,7 +43,8 @@ $(OUT)/rsexercise: $(REFERENCE)/rsexercise.C $(REFERENCE)/exercise.H $(ROOT)/inc
 # rsvalidate, rsspeed and rstest: the programs that need libfec's headers, built in one recipe around
 # one temporary unpack of the tarball
 $(OUT)/.karn_stamp: $(REFERENCE)/rsvalidate.C $(REFERENCE)/rsspeed.C $(REFERENCE)/phil-karn/rstest.c $(KEX) \
-                    $(TGZ) $(ROOT)/include/ezpwd_amd/rs $(LIB)/libezrs_fec.so $(HERE)harness.mk
+                    $(TGZ) $(ROOT)/include/ezpwd_amd/rs $(LIB)/libezrs_fec.so $(HERE)harness.mk \
+                    $(if $(KARN_MISSING),FORCE)
 	@mkdir -p $(OUT)
 	@rm -rf $(OUT)/.fec $(OUT)/.o
 	T=$$(mktemp -d /tmp/ezrs_fec.XXXXXX) && ( set -e; \

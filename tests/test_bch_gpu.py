@@ -287,3 +287,38 @@ def test_decode_syn_host_form(torch):
         assert res[k] == er
         if er > 0:
             np.testing.assert_array_equal(loc[k, :er], el)
+
+
+def test_c5_packed_rows_at_odd_offset(torch):
+    """the C5 decode's write-back of corrected 16-byte pieces when the rows' base is not
+    16-byte aligned (a view at byte offset 3 of packed 127-byte rows): the row base's misalignment
+    and the edge pieces written byte by byte.  Errors in the first and last rows of every 64-row
+    wave and in random others; bytes outside the rows must stay untouched."""
+    import ezrs
+    oc, c = O.BCH(10, 4), ezrs.BCH.nkt(1023, 983, 4)
+    L, eb = 122, 5
+    ncw = 5000
+    rng = np.random.default_rng(0xB5)
+    rows = rng.integers(0, 256, (ncw, L + eb), dtype=np.uint8)
+    oc.encode_batch(rows, L, nthreads=8)
+    bad = rows.copy()
+    counts = np.zeros(ncw, np.int64)
+    k = np.arange(ncw)
+    counts[(k % 64 == 0) | (k % 64 == 63)] = 4
+    counts[rng.choice(ncw, 800, replace=False)] = rng.integers(1, 5, 800)
+    _flip(bad, 8 * L + oc.ecc_bits, counts, rng)
+    exp = bad.copy()
+    eres = oc.decode_batch(exp, L, nthreads=8)
+    for off in (3, 9):
+        flat = torch.from_numpy(rng.integers(0, 256, ncw * (L + eb) + 32, dtype=np.uint8)).cuda()
+        guard = flat.clone()
+        view = flat[off:off + ncw * (L + eb)].view(ncw, L + eb)
+        view.copy_(torch.from_numpy(bad).cuda())
+        res = c.decode(view, L).cpu().numpy()
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(res, eres, err_msg=f"result off={off}")
+        np.testing.assert_array_equal(view.cpu().numpy(), exp, err_msg=f"rows off={off}")
+        f = flat.cpu().numpy()
+        g = guard.cpu().numpy()
+        np.testing.assert_array_equal(f[:off], g[:off])
+        np.testing.assert_array_equal(f[off + ncw * (L + eb):], g[off + ncw * (L + eb):])

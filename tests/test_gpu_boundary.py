@@ -157,3 +157,29 @@ def test_decode_host_single_codeword_zero_eras_stride(torch):
     assert rc == 0 and res[0] == 3
     np.testing.assert_array_equal(row, good)
     assert sorted(pos[:3].tolist()) == [5, 77, 200]
+
+
+def test_decode_null_eras_with_stride(torch):
+    """eras = NULL with a nonzero eras_stride: the error path must not read erasures
+    (the 16-byte erasure preload is gated on a non-null list), and a corrupted codeword among clean
+    ones is still corrected exactly as the oracle does."""
+    import ezrs
+    L = ezrs.lib()
+    c = ezrs.Codec.rs(255, 223)
+    oc = O.Codec(*O.rs_params(255, 223))
+    rng = np.random.default_rng(0xE5)
+    ncw = 300
+    h = _batch(rng, ncw)
+    oc.encode_batch(h, 223)
+    good = h.copy()
+    h[17, [3, 99, 250]] ^= np.array([0x11, 0x22, 0x33], np.uint8)
+    exp = oc.decode_batch(h.copy(), 223)
+    d = torch.from_numpy(h).cuda()
+    res = torch.empty(ncw, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    assert L.ezrs_decode(c._h, C.c_void_p(d.data_ptr()), 255, 223, None, 0, None, 32, None,
+                         C.c_void_p(res.data_ptr()), None, 0, None, 0, ncw, C.c_void_p(s)) == 0
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(res.cpu().numpy(), exp)
+    assert res.cpu().numpy()[17] == 3
+    np.testing.assert_array_equal(d.cpu().numpy(), good)

@@ -204,7 +204,8 @@ def test_device_karn_corrections(fec, case):
     """Corrections (`corr`) of a Karn-mode device decode: for every root in the data or parity the
     value XORed into the row (libfec's in/out difference at that position; an entry is left alone
     where the error value is zero), for a root in the pad (counted but not corrected,
-    decode_rs.h:277-289) zero, or left alone when its error value is zero."""
+    decode_rs.h:277-289) exactly zero (include/ezrs.h documents it), and left alone
+    where a data / parity root's error value is zero."""
     import torch
     import ezrs
     m, poly, fcr, prim, nr = case["params"]
@@ -228,7 +229,7 @@ def test_device_karn_corrections(fec, case):
             p = int(pos[k, j])                          # full-frame position
             if p < pad:
                 npad += 1
-                assert corr[k, j] in (0, 0xEE), f"cw {k} root {j} in the pad"
+                assert corr[k, j] == 0, f"cw {k} root {j} in the pad"   # include/ezrs.h: zero
             else:                                       # (0xEE also: a zero error value, not written)
                 d = diff[k, p - pad]
                 assert corr[k, j] == d or (corr[k, j] == 0xEE and d == 0), f"cw {k} root {j}"

@@ -2,7 +2,7 @@
 // EZRS_PS_STAMPS): s_memtime at each phase boundary of every workgroup's first 9 tiles, and
 // s_memrealtime + s_memtime at each workgroup's start and end (its clock).  Decode runs on 1 M valid
 // RS(255,223) codewords (random data encoded on the host: the clean C2 case); encode on random data.
-// Usage: pq_stamps [enc] [2]   (2: the double-buffered kernel k_pq2)
+// Usage: pq_stamps [enc]
 #define EZRS_PS_STAMPS 1
 #include "../../ezpwd-reed-solomon_amd/csrc/ezrs_ps.hip"
 #include <algorithm>
@@ -24,7 +24,6 @@ static void host_encode(uint8_t *cw, const uint8_t *A, const uint8_t *L, const u
 
 int main(int argc, char **argv) {
     const int enc = argc > 1 ? atoi(argv[1]) : 0;
-    const bool two = argc > 2 && atoi(argv[2]) == 2;
     const size_t ncw = 1u << 20;
     uint8_t A[256], L[256];
     for (int i = 0, x = 1; i < 255; ++i) { A[i] = (uint8_t)x; L[x] = (uint8_t)i; x <<= 1; if (x & 256) x ^= 0x11d; }
@@ -57,10 +56,7 @@ int main(int argc, char **argv) {
     for (int rep = 0; rep < 60; ++rep) {
         hipEvent_t a, b; (void)hipEventCreate(&a); (void)hipEventCreate(&b);
         (void)hipEventRecord(a);
-        if (two) {
-            if (enc) hipLaunchKernelGGL((ps::pq2::k_pq2<ps::PQ_RS_255_223, true>), dim3(grid), dim3(256), 0, 0, p);
-            else hipLaunchKernelGGL((ps::pq2::k_pq2<ps::PQ_RS_255_223, false>), dim3(grid), dim3(256), 0, 0, p);
-        } else if (enc) hipLaunchKernelGGL((ps::pq::k_pq_lin<ps::PQ_RS_255_223, true, false, true>), dim3(grid), dim3(256), 0, 0, p);
+        if (enc) hipLaunchKernelGGL((ps::pq::k_pq_lin<ps::PQ_RS_255_223, true, false, true>), dim3(grid), dim3(256), 0, 0, p);
         else hipLaunchKernelGGL((ps::pq::k_pq_lin<ps::PQ_RS_255_223, false, false, true>), dim3(grid), dim3(256), 0, 0, p);
         (void)hipEventRecord(b); (void)hipEventSynchronize(b);
         float ms; (void)hipEventElapsedTime(&ms, a, b);
@@ -77,10 +73,8 @@ int main(int argc, char **argv) {
     static unsigned long long stp[512][4][9][8], rt[512][4];
     (void)hipMemcpyFromSymbol(stp, HIP_SYMBOL(ps::g_pq_stamps), sizeof stp);
     (void)hipMemcpyFromSymbol(rt, HIP_SYMBOL(ps::g_pq_rt), sizeof rt);
-    const char *names1[] = {"dma+bar", "main", "bar", "xchg", "fold", "st", "next", ""};
-    const char *names2[] = {"wait0", "mainA", "wait1", "mainB", "bar", "xchg", "fold", "st"};
-    const char **names = two ? names2 : names1;
-    const int nph = two ? 7 : 6;                                  // phases within a tile
+    const char *names[] = {"dma+bar", "main", "bar", "xchg", "fold", "st", "next", ""};
+    const int nph = 6;                                            // phases within a tile
     // per-workgroup duration and clock
     std::vector<double> dur, clk;
     unsigned long long t0 = ~0ull, t1 = 0;
