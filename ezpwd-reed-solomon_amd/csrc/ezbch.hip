@@ -33,7 +33,13 @@
 #include <vector>
 
 #include "../../include/ezbch.h"
+#include "ezbch_ps.hpp"
 #include "ezrs_internal.hpp"
+
+using ezrs::BpsArgs;
+using ezrs::bps_codec_id;
+using ezrs::bps_frame;
+using ezrs::launch_bps;
 
 namespace {
 
@@ -54,6 +60,8 @@ struct DevBch {
     const uint16_t *lg;       // [n+1] log_alpha (lg[0] unused)
     const uint64_t *syn_tab;  // ecc_bits <= 64, t <= 4: [8][256] the odd syndromes S1, S3, S5, S7
                               // (16 bits each) of remainder byte b (from the top) holding value v
+    int bps;                  // plane-sliced remainder kernels (ezbch_ps.hip): codec id, or -1
+    int ncu;                  // compute units of the device
 };
 
 struct BchArgs {
@@ -1100,7 +1108,39 @@ BchArgs wave_chunk(const BchArgs &a, size_t k0) {
     return c;
 }
 
+// Launches of the plane-sliced kernels over a batch: 256-row tiles, every byte offset of a launch
+// below 0xE0000000 (32-bit buffer offsets).
+template <class F>
+hipError_t bps_chunks(const BchArgs &a, F &&launch) {
+    size_t per = (size_t)0xE0000000u / (a.dstride ? a.dstride : 1) / 256 * 256;
+    if (per == 0) per = 256;
+    for (size_t k0 = 0; k0 < a.ncw; k0 += per) {
+        const size_t n = a.ncw - k0 < per ? a.ncw - k0 : per;
+        const hipError_t e = launch(k0, n);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+// The plane-sliced path takes rows of its frame (data + ECC <= F bytes) at a pitch of at most 128
+// bytes; decode also needs the ECC right after the data (the row is one polynomial).
+bool bps_ok(const DevBch &b, const BchArgs &a, bool dec) {
+    if (b.bps < 0 || a.ecc_only || a.syn || a.len == 0 || a.dstride > 128 || a.ncw == 0) return false;
+    if (8ull * a.len > (unsigned long long)(b.n - b.ecc_bits)) return false;
+    if ((int)(a.len + b.ecc_bytes) > bps_frame(b.bps)) return false;
+    if (dec && !(a.ecc == a.data + a.len && a.estride == a.dstride)) return false;
+    return a.dstride >= a.len;
+}
+
 hipError_t launch_encode(const DevBch &b, BchArgs a, hipStream_t s) {
+    if (bps_ok(b, a, false)) {
+        return bps_chunks(a, [&](size_t k0, size_t n) {
+            const BpsArgs p{a.data + k0 * a.dstride, (uint32_t)((n - 1) * a.dstride + a.len), (uint32_t)a.dstride,
+                            (uint32_t)n, (uint32_t)((n + 255) / 256), bps_frame(b.bps) - (int)(a.len + b.ecc_bytes),
+                            a.ecc + k0 * a.estride, a.estride, nullptr, nullptr};
+            return launch_bps(b.bps, false, p, b.ncu, s);
+        });
+    }
     if (b.nwl) {
         for (size_t k0 = 0; k0 < a.ncw; k0 += kWaveChunk) {      // one workgroup per codeword
             const BchArgs c = wave_chunk(a, k0);
@@ -1375,6 +1415,9 @@ int create_impl(ezbch_codec **out, unsigned m, unsigned t, unsigned poly, int de
         }
         d.syn_tab = c->d_syn;
     }
+    d.bps = !d.nwl && c->h.ecc_bits % 8 == 0 && c->h.poly == kDefaultPoly[m - 5]
+                ? bps_codec_id((int)m, (int)t, (int)c->h.ecc_bits) : -1;
+    if (hipDeviceGetAttribute(&d.ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) d.ncu = 256;
     *out = c;
     return 0;
 }

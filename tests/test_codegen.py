@@ -26,9 +26,37 @@ def _load(name):
 
 @pytest.mark.parametrize("gen,inc", [("gen_bitslice", "ezrs_bs_tables.inc"),
                                      ("gen_ps", "ezrs_ps_tables.inc"),
-                                     ("gen_wide", "ezrs_wide_tables.inc")])
+                                     ("gen_wide", "ezrs_wide_tables.inc"),
+                                     ("gen_bch_ps", "ezbch_ps_tables.inc")])
 def test_generated_tables_are_reproduced(tmp_path, gen, inc):
     dst = str(tmp_path / inc)
     _load(gen).main(dst)
     assert filecmp.cmp(dst, os.path.join(GEN, inc), shallow=False), \
         f"csrc/gen/{inc} differs from codegen/{gen}.py's output: regenerate it"
+
+
+@pytest.mark.parametrize("name,m,t", [("BCH_10_4", 10, 4), ("BCH_8_2", 8, 2)])
+def test_bch_plane_decomposition_matches_oracle(name, m, t):
+    """gen_bch_ps.py's algebra (weights w(q) = x^(8q) mod g, planes folded as sum_b x^b U_b) gives
+    the oracle's encode_bch ECC, left-justified big-endian, for random rows of ragged lengths."""
+    import numpy as np
+    import oracle
+    gen = _load("gen_bch_ps")
+    c = gen.BpsCodec(name, m, t)
+    ref = oracle.BCH(m, t)
+    assert (c.E, c.EB) == (ref.ecc_bits, ref.ecc_bytes)
+    rng = np.random.default_rng(m * 100 + t)
+    for L in (1, 2, 7, c.max_len // 2, c.max_len):
+        row = rng.integers(0, 256, L, dtype=np.uint8)
+        frame = [0] * c.F                       # right-aligned: data then EB zero ECC bytes
+        frame[c.F - c.EB - L:c.F - c.EB] = row.tolist()
+        U = [0] * 8
+        for f, byte in enumerate(frame):
+            for b in range(8):
+                if (byte >> b) & 1:
+                    U[b] ^= c.w(c.F - 1 - f)
+        r = 0
+        for b in range(8):
+            r ^= gen.polymod(U[b] << b, c.g, c.E)
+        ecc = (r << (8 * c.EB - c.E)).to_bytes(c.EB, "big")
+        assert ecc == bytes(ref.encode(row)), (name, L)
