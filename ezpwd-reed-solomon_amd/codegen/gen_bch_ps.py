@@ -18,10 +18,11 @@ Fold: sum_b x^b U_b in three levels inside each byte (planes 2m + x plane 2m+1, 
 x^4: shift the word by 1, 2, 4 and multiply by x^s mod g, a sparse E x E map), leaving remainder
 bit i of row k at bit 8k of U[i].
 
-Frame: F byte positions, the row right-aligned (its last byte at position F - 1, q = F - 1 - f).
-Encode reads the data (ECC positions masked to zero), decode the data and the received ECC: the
-remainder of the whole row is then the data's remainder XOR the received ECC, the difference
-decode_bch works from.  Codecs: E a multiple of 8 (ECC bytes exactly E / 8), E <= 64.
+Frame: F byte positions, right-aligned: position F - 1 holds the byte Q0 places from the row's end
+(q = F - 1 - f + Q0).  Encode reads the data alone (Q0 = ECC bytes: the ECC positions that follow
+are zero), decode the data and the received ECC (Q0 = 0): the remainder of the whole row is then
+the data's remainder XOR the received ECC, the difference decode_bch works from.  Codecs: E a
+multiple of 8 (ECC bytes exactly E / 8), E <= 64.
 """
 from __future__ import annotations
 
@@ -132,19 +133,20 @@ def gen_codec(c: BpsCodec):
     out = [f"struct {st} {{",
            f"    static constexpr int M = {c.m}, T = {c.t}, E = {E}, EB = {c.EB}, F = {F}, NB = {NB};",
            f"    static constexpr unsigned G_LO = {c.g & 0xffffffff:#x}u, POLY = {c.poly:#x};",
-           "    // frame block B (byte positions 8B .. 8B+7, words X) into the state (FIRST: set it)",
-           "    template <int B, bool FIRST> static __device__ void block(uint32_t (&U)[E], const uint32_t (&X)[8]);",
+           "    // frame block B (byte positions 8B .. 8B+7, words X) into the state (FIRST: set it);",
+           "    // position F - 1 is the byte Q0 places from the row's end (encode Q0 = EB, decode 0)",
+           "    template <int B, bool FIRST, int Q0>",
+           "    static __device__ void block(uint32_t (&U)[E], const uint32_t (&X)[8]);",
            "    // sum_b x^b U_b: remainder bit i of row k left at bit 8k of U[i]",
            "    static __device__ void fold(uint32_t (&U)[E]);",
            "};"]
     I = "    "
-    for B in range(NB):
-        for first in (True, False):
-            out.append(f"template <> __device__ __forceinline__ void {st}::block<{B}, {str(first).lower()}>("
+    for q0, B, first in ((q0, B, first) for q0 in (c.EB, 0) for B in range(NB) for first in (True, False)):
+            out.append(f"template <> __device__ __forceinline__ void {st}::block<{B}, {str(first).lower()}, {q0}>("
                        "uint32_t (&U)[E], const uint32_t (&X)[8]) {")
             emit_combos(out, "l", [f"X[{t}]" for t in range(4)], I)
             emit_combos(out, "h", [f"X[{t}]" for t in range(4, 8)], I)
-            ws = [c.w(F - 1 - (8 * B + t)) for t in range(8)]
+            ws = [c.w(F - 1 - (8 * B + t) + q0) for t in range(8)]
             for k in range(E):
                 m1 = sum(((ws[t] >> k) & 1) << t for t in range(4))
                 m2 = sum(((ws[4 + t] >> k) & 1) << t for t in range(4))

@@ -33,7 +33,7 @@
 #include <vector>
 
 #include "../../include/ezbch.h"
-#include "ezbch_ps.hpp"
+#include "ezbch_ps_tile.hpp"
 #include "ezrs_internal.hpp"
 
 using ezrs::BpsArgs;
@@ -646,6 +646,98 @@ __global__ void __launch_bounds__(kThreads) k_bch_decode(DevBch b, BchArgs a) {
     write_pieces<T>(rows, row, loc, cnt, b, a);
 }
 
+// ---- plane-sliced codecs, ECC inline (C5): the fused decode ------------------------------------
+// The encode's tile loop (ezbch_ps_tile.hpp) leaves each row's remainder XOR its received ECC in
+// registers; a nonzero one is located (locate<T, 1>, the GF tables staged in LDS), its bits are
+// flipped in the tile's LDS image, and after a workgroup barrier each row writes back the 16-byte
+// pieces of the global grid that hold its flips -- a piece reaching outside the tile's bytes only
+// over the tile's own, byte by byte.  One pass over the rows: read once, corrected pieces written.
+template <class C>
+__global__ void __launch_bounds__(64 * ezrs::bps::kTW) k_bch_ps_decode(DevBch b, BchArgs a, BpsArgs p) {
+    namespace bp = ezrs::bps;
+    constexpr int TW = bp::tile_waves<C>(), T = C::T, NR = 4 / TW;
+    constexpr uint32_t n = (1u << C::M) - 1;
+    static_assert(T <= 4, "odd syndromes S1 .. S7 from the nibble tables");
+    constexpr uint32_t kTabs = ((3 * n + 1) * 2 + 15) / 16 * 16, kNib = 2 * C::EB * 16;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[bp::kLds + kTabs + 8 * kNib];
+    uint16_t *ex = reinterpret_cast<uint16_t *>(lds + bp::kLds), *lg = ex + 2 * n;
+    // syndrome tables by nibble of the remainder (from the top): the byte tables are linear in the
+    // byte, so nibble q's entry for v is the byte table's for v << 4 (q even) or v
+    uint64_t *nib = reinterpret_cast<uint64_t *>(lds + bp::kLds + kTabs);
+    for (uint32_t i = threadIdx.x; i < 2 * n; i += blockDim.x) ex[i] = b.ex[i];
+    for (uint32_t i = threadIdx.x; i <= n; i += blockDim.x) lg[i] = b.lg[i];
+    for (uint32_t i = threadIdx.x; i < kNib; i += blockDim.x) {
+        const uint32_t q = i >> 4, v = i & 15u;
+        nib[i] = b.syn_tab[(q >> 1) * 256 + ((q & 1) ? v : v << 4)];
+    }
+    __syncthreads();
+    const GF f{ex, lg, (int)n};
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = bp::lane_id();
+    const uint32_t nbits = 8u * a.len + (uint32_t)b.ecc_bits, tb = bp::kRows * p.stride;
+    // rows 4l + k, k = w (TW = 4) or 2w, 2w + 1
+    bp::tile_loop<C, true, -1>(p, lds, [&](uint32_t tile, uint8_t *image, const uint32_t (&out)[C::EB]) {
+        uint32_t loc[NR][T];
+        int cnt[NR];
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+            const uint32_t k = NR * w + j, r = 4u * l + k;
+            const size_t row = (size_t)tile * bp::kRows + r;
+            cnt[j] = 0;
+            if (row >= a.ncw) continue;
+            uint32_t wd[2];
+            bp::row_bytes<C::EB>(out, k, wd);
+            Rem<1> rm;
+            rm.w[0] = (((uint64_t)__builtin_bswap32(wd[0]) << 32) | __builtin_bswap32(wd[1])) & b.emask[0];
+            int c = 0;
+            if (rm.w[0]) {
+                uint64_t acc = 0;
+#pragma unroll
+                for (uint32_t q = 0; q < 2 * C::EB; ++q) acc ^= nib[q * 16 + (uint32_t)((rm.w[0] >> (60 - 4 * q)) & 15u)];
+                uint32_t S[2 * T];                          // S_1 .. S_2T; S_2j = S_j^2
+#pragma unroll
+                for (int jj = 1; jj < 2 * T; jj += 2) S[jj - 1] = (uint32_t)(acc >> (8 * (jj - 1))) & 0xFFFFu;
+#pragma unroll
+                for (int jj = 1; jj <= T; ++jj) S[2 * jj - 1] = f.sq(S[jj - 1]);
+                c = locate<T, 1>(b, f, rm, nbits, loc[j], S);
+            }
+            a.result[row] = c;
+            if (c <= 0) continue;
+            cnt[j] = c;
+#pragma unroll
+            for (int i = 0; i < T; ++i) {
+                if (i >= c) break;
+                if (a.errloc) a.errloc[row * a.lstride + i] = loc[j][i];
+                const uint32_t o = r * p.stride + (loc[j][i] >> 3);
+                atomicXor(reinterpret_cast<uint32_t *>(image + (o & ~3u)), (1u << (loc[j][i] & 7)) << (8 * (o & 3)));
+            }
+        }
+        __syncthreads();                                    // every row's flips are in the image
+        const uint32_t toff = tile * tb, hi = p.span - toff < tb ? p.span - toff : tb;
+        uint8_t *g = a.wdata + toff;                        // image byte 0
+        const uint32_t gmis = (uint32_t)((uintptr_t)g & 15u);
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+            const uint32_t r = 4u * l + NR * w + j;
+            int last = -1000;
+#pragma unroll
+            for (int i = 0; i < T; ++i) {
+                if (i >= cnt[j]) break;
+                const uint32_t o = r * p.stride + (loc[j][i] >> 3);
+                const int p0 = (int)((o + gmis) & ~15u) - (int)gmis;   // image offset of the piece
+                if (p0 == last) continue;
+                last = p0;
+                if (p0 >= 0 && p0 + 16 <= (int)hi) {
+                    uint4 v;
+                    __builtin_memcpy(&v, image + p0, 16);
+                    *reinterpret_cast<uint4 *>(g + p0) = v;
+                } else {
+                    for (int q = p0 < 0 ? 0 : p0; q < p0 + 16 && q < (int)hi; ++q) g[q] = image[q];
+                }
+            }
+        }
+    });
+}
+
 // ---- t > 16 or ecc_bits > 256: the same decode with run-time t ------------------------------
 // The working polynomials are per-lane arrays indexed at run time (scratch memory): slower than
 // the register-resident k_bch_decode<T, NW>, for the codecs it does not instantiate.
@@ -1112,7 +1204,9 @@ BchArgs wave_chunk(const BchArgs &a, size_t k0) {
 // below 0xE0000000 (32-bit buffer offsets).
 template <class F>
 hipError_t bps_chunks(const BchArgs &a, F &&launch) {
-    size_t per = (size_t)0xE0000000u / (a.dstride ? a.dstride : 1) / 256 * 256;
+    const size_t pitch = a.dstride > a.estride ? a.dstride : a.estride;
+    size_t per = (size_t)0xE0000000u / (pitch ? pitch : 1) / 256 * 256;
+    if (per > ((size_t)1 << 28)) per = (size_t)1 << 28;       // 8-byte remainders: 32-bit offsets
     if (per == 0) per = 256;
     for (size_t k0 = 0; k0 < a.ncw; k0 += per) {
         const size_t n = a.ncw - k0 < per ? a.ncw - k0 : per;
@@ -1122,13 +1216,15 @@ hipError_t bps_chunks(const BchArgs &a, F &&launch) {
     return hipSuccess;
 }
 
-// The plane-sliced path takes rows of its frame (data + ECC <= F bytes) at a pitch of at most 128
-// bytes; decode also needs the ECC right after the data (the row is one polynomial).
+// The plane-sliced path takes rows of its frame (encode: data <= F bytes, decode: data + ECC) at a
+// pitch of at most 128 bytes; decode also needs the ECC right after the data (the row is one
+// polynomial).
 bool bps_ok(const DevBch &b, const BchArgs &a, bool dec) {
     if (b.bps < 0 || a.ecc_only || a.syn || a.len == 0 || a.dstride > 128 || a.ncw == 0) return false;
     if (8ull * a.len > (unsigned long long)(b.n - b.ecc_bits)) return false;
-    if ((int)(a.len + b.ecc_bytes) > bps_frame(b.bps)) return false;
+    if ((int)(a.len + (dec ? b.ecc_bytes : 0)) > bps_frame(b.bps)) return false;
     if (dec && !(a.ecc == a.data + a.len && a.estride == a.dstride)) return false;
+    if (!dec && (a.estride < b.ecc_bytes || a.estride > 4096)) return false;
     return a.dstride >= a.len;
 }
 
@@ -1136,9 +1232,10 @@ hipError_t launch_encode(const DevBch &b, BchArgs a, hipStream_t s) {
     if (bps_ok(b, a, false)) {
         return bps_chunks(a, [&](size_t k0, size_t n) {
             const BpsArgs p{a.data + k0 * a.dstride, (uint32_t)((n - 1) * a.dstride + a.len), (uint32_t)a.dstride,
-                            (uint32_t)n, (uint32_t)((n + 255) / 256), bps_frame(b.bps) - (int)(a.len + b.ecc_bytes),
-                            a.ecc + k0 * a.estride, a.estride, nullptr, nullptr};
-            return launch_bps(b.bps, false, p, b.ncu, s);
+                            (uint32_t)n, (uint32_t)((n + 255) / 256), bps_frame(b.bps) - (int)a.len,
+                            a.ecc + k0 * a.estride, a.estride,
+                            (uint32_t)((n - 1) * a.estride + b.ecc_bytes)};
+            return launch_bps(b.bps, p, b.ncu, s);
         });
     }
     if (b.nwl) {
@@ -1165,7 +1262,36 @@ hipError_t launch_encode(const DevBch &b, BchArgs a, hipStream_t s) {
     return hipGetLastError();
 }
 
+hipError_t launch_bps_decode(const DevBch &b, const BchArgs &a, const BpsArgs &p, hipStream_t s) {
+    const unsigned cap = 2u * (unsigned)(b.ncu > 0 ? b.ncu : 256);         // 2 workgroups per CU (LDS)
+    const unsigned grid = p.ntiles < cap ? p.ntiles : cap;
+    if (!grid) return hipSuccess;
+    int k = 0;
+#define EZBCH_PS_DECODE(N, M, T)                                                                     \
+    if (k++ == b.bps)                                                                                \
+        hipLaunchKernelGGL((k_bch_ps_decode<ezrs::bps::BPS_##N>), dim3(grid),                       \
+                           dim3(64 * ezrs::bps::tile_waves<ezrs::bps::BPS_##N>()), 0, s, b, a, p);
+    EZBCH_PS_CODEC_LIST(EZBCH_PS_DECODE)
+#undef EZBCH_PS_DECODE
+    return hipGetLastError();
+}
+
 hipError_t launch_decode(const DevBch &b, BchArgs a, hipStream_t s) {
+    if (bps_ok(b, a, true) && ecc_inline(b, a)) {            // packed rows, ECC inline: fused decode
+        return bps_chunks(a, [&](size_t k0, size_t n) {
+            BchArgs c = a;
+            c.ncw = n;
+            c.data += k0 * a.dstride;
+            c.wdata += k0 * a.dstride;
+            c.ecc += k0 * a.estride;
+            c.result += k0;
+            if (c.errloc) c.errloc += k0 * a.lstride;
+            const BpsArgs p{c.data, (uint32_t)((n - 1) * a.dstride + a.len + b.ecc_bytes), (uint32_t)a.dstride,
+                            (uint32_t)n, (uint32_t)((n + 255) / 256), bps_frame(b.bps) - (int)(a.len + b.ecc_bytes),
+                            nullptr, 0, 0};
+            return launch_bps_decode(b, c, p, s);
+        });
+    }
     if (b.nwl) {
         const size_t sh = wave_lds_bytes(b.t);
         for (size_t k0 = 0; k0 < a.ncw; k0 += kWaveChunk) {      // one workgroup per codeword

@@ -38,7 +38,8 @@ def test_generated_tables_are_reproduced(tmp_path, gen, inc):
 @pytest.mark.parametrize("name,m,t", [("BCH_10_4", 10, 4), ("BCH_8_2", 8, 2)])
 def test_bch_plane_decomposition_matches_oracle(name, m, t):
     """gen_bch_ps.py's algebra (weights w(q) = x^(8q) mod g, planes folded as sum_b x^b U_b) gives
-    the oracle's encode_bch ECC, left-justified big-endian, for random rows of ragged lengths."""
+    the oracle's encode_bch ECC, left-justified big-endian, for random rows of ragged lengths in
+    the encode frame, and a zero remainder for the codeword in the decode frame."""
     import numpy as np
     import oracle
     gen = _load("gen_bch_ps")
@@ -48,15 +49,19 @@ def test_bch_plane_decomposition_matches_oracle(name, m, t):
     rng = np.random.default_rng(m * 100 + t)
     for L in (1, 2, 7, c.max_len // 2, c.max_len):
         row = rng.integers(0, 256, L, dtype=np.uint8)
-        frame = [0] * c.F                       # right-aligned: data then EB zero ECC bytes
-        frame[c.F - c.EB - L:c.F - c.EB] = row.tolist()
-        U = [0] * 8
-        for f, byte in enumerate(frame):
+        ecc_ref = bytes(ref.encode(row))
+        # encode frame: the data right-aligned, position F - 1 = EB bytes before the row's end;
+        # decode frame: data + ECC right-aligned (Q0 = 0), remainder 0 for a codeword
+        for q0, frame_bytes, want in ((c.EB, row.tolist(), ecc_ref),
+                                      (0, row.tolist() + list(ecc_ref), bytes(c.EB))):
+            frame = [0] * (c.F - len(frame_bytes)) + frame_bytes
+            U = [0] * 8
+            for f, byte in enumerate(frame):
+                for b in range(8):
+                    if (byte >> b) & 1:
+                        U[b] ^= c.w(c.F - 1 - f + q0)
+            r = 0
             for b in range(8):
-                if (byte >> b) & 1:
-                    U[b] ^= c.w(c.F - 1 - f)
-        r = 0
-        for b in range(8):
-            r ^= gen.polymod(U[b] << b, c.g, c.E)
-        ecc = (r << (8 * c.EB - c.E)).to_bytes(c.EB, "big")
-        assert ecc == bytes(ref.encode(row)), (name, L)
+                r ^= gen.polymod(U[b] << b, c.g, c.E)
+            got = (r << (8 * c.EB - c.E)).to_bytes(c.EB, "big")
+            assert got == want, (name, L, q0)

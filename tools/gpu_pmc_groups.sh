@@ -1,20 +1,18 @@
 #!/bin/bash
-# Instruction-fetch / issue counters of the C2 kernels: lists the gfx950 counters once, then one
-# rocprofv3 --pmc pass per group (counters the box does not have are dropped from the group), then
-# a per-kernel summary.  Usage: [KFILT=regex] tools/gpu_icache.sh <tag> [extra bench args]
+# PMC passes (one rocprofv3 --pmc run per group; counters the box lacks are dropped) over a short
+# bench run, then a per-kernel summary of the kernels matching KFILT.
+# Usage: KFILT=regex tools/gpu_pmc_groups.sh <tag> "<group1>" "<group2>" ... -- [bench args]
 set -u
-TAG=${1:-icache}; shift || true
+TAG=$1; shift
+GROUPS_=()
+while [ $# -gt 0 ] && [ "$1" != "--" ]; do GROUPS_+=("$1"); shift; done
+[ $# -gt 0 ] && shift
 OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp
 timeout -s KILL 60 rocprofv3 -L > $OUT/counters.txt 2>&1 || true
-have() { grep -qw "$1" $OUT/counters.txt; }
-GROUPS_=(
-  "SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH"
-  "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_BUSY_CYCLES"
-  "SQ_IFETCH_LEVEL SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS"
-)
+have() { grep -qw "$1" $OUT/counters.txt || [ "$1" = FETCH_SIZE ] || [ "$1" = WRITE_SIZE ]; }
 i=0
 for grp in "${GROUPS_[@]}"; do
   i=$((i+1))
@@ -29,18 +27,21 @@ for grp in "${GROUPS_[@]}"; do
   echo "== pass $i rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 $OUT/p$i.log; exit $rc; fi
 done
-python3 - $OUT "${KFILT:-pq_lin|parity}" <<'EOF'
+python3 - $OUT "${KFILT:-.}" <<'PY'
 import csv, glob, re, sys, collections
 out, kf = sys.argv[1], re.compile(sys.argv[2])
 acc = collections.defaultdict(lambda: collections.defaultdict(float))
+calls = collections.defaultdict(set)
 for f in glob.glob(out + "/p*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        acc[r["Kernel_Name"][:80]][r["Counter_Name"]] += float(r["Counter_Value"])
+        k = r["Kernel_Name"][:80]
+        acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
+        calls[k].add((f, r.get("Dispatch_Id", "")))
 for k, d in acc.items():
     if not kf.search(k):
         continue
     print(k)
     for c, v in sorted(d.items()):
         print(f"   {c:28s} {v:12.4g}")
-EOF
+PY
 exit 0
