@@ -20,8 +20,8 @@ CALLS = {
     "ezrs_encode": ("k_py_syndromes<", "true>", "k_ps_parity", "k_wide_rem", "k_wide_finish<true>"),
     "ezrs_decode": ("k_py_syndromes<", "false>", "k_decode_errors", "k_wide_rem", "k_wide_finish<false>",
                     "k_wide_errors"),
-    "ezbch_encode": ("k_bch_encode",),
-    "ezbch_decode": ("k_bch_decode",),
+    "ezbch_encode": ("k_bch_encode", "k_bch_ps<"),
+    "ezbch_decode": ("k_bch_decode", "k_bch_ps_decode"),
 }
 
 
@@ -31,6 +31,10 @@ def kernel_call(name):
             return "ezrs_encode" if name.split(kn)[1].split(",")[1].strip() == "true" else "ezrs_decode"
     if "k_py_syndromes" in name or "k_pg_syndromes" in name:
         return "ezrs_encode" if "true>" in name else "ezrs_decode"
+    if "k_bch_ps_decode" in name:
+        return "ezbch_decode"
+    if "k_bch_ps<" in name:
+        return "ezbch_encode"
     for call, keys in (("ezrs_encode", ("k_ps_parity", "k_wide_finish<true>")),
                        ("ezrs_decode", ("k_decode_errors", "k_wide_finish<false>", "k_wide_errors")),
                        ("ezbch_encode", ("k_bch_encode",)), ("ezbch_decode", ("k_bch_decode",))):
