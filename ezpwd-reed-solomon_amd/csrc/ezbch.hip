@@ -266,7 +266,7 @@ __device__ int solve_affine(const GF &f, int m, uint32_t A4, uint32_t A2, uint32
     uint32_t v[kMaxM], c[kMaxM];
     int pb[kMaxM];
     int dim = 0;
-    k1 = k2 = 0;
+    uint32_t q1 = 0, q2 = 0;                // k1, k2: selects, not a store indexed by dim (scratch)
 #pragma unroll
     for (int i = 0; i < kMaxM; ++i) {
         v[i] = 0;
@@ -286,13 +286,10 @@ __device__ int solve_affine(const GF &f, int m, uint32_t A4, uint32_t A2, uint32
                 }
             v[i] = w;
             c[i] = cc;
-            if (w) {
-                pb[i] = 31 - __clz(w);
-            } else {
-                if (dim == 0) k1 = cc;
-                else if (dim == 1) k2 = cc;
-                ++dim;
-            }
+            pb[i] = w ? 31 - __clz(w) : -1;
+            q1 = (!w && dim == 0) ? cc : q1;
+            q2 = (!w && dim == 1) ? cc : q2;
+            dim += !w;
         }
     }
     uint32_t y = 0, rem = delta;
@@ -303,6 +300,8 @@ __device__ int solve_affine(const GF &f, int m, uint32_t A4, uint32_t A2, uint32
             y ^= c[k];
         }
     y0 = y;
+    k1 = q1;
+    k2 = q2;
     return rem ? -1 : dim;
 }
 
@@ -328,21 +327,14 @@ __device__ int small_roots(const GF &f, int m, int L, uint32_t a, uint32_t b, ui
     }
     uint32_t y0, k1, k2;
     if (solve_affine(f, m, A4, A2, A1, delta, y0, k1, k2) != want) return 0;
-    if (L == 2) {
-        X[0] = y0;
-        X[1] = y0 ^ k1;
-        return 2;
-    }
-    if (L == 3) {                           // y0 = 0: the three nonzero kernel elements
-        X[0] = k1 ^ s;
-        X[1] = k2 ^ s;
-        X[2] = k1 ^ k2 ^ s;
-        return 3;
-    }
-    const uint32_t y[4] = {y0, y0 ^ k1, y0 ^ k2, y0 ^ k1 ^ k2};
+    // L = 2: y0, y0 + k1; L = 3 (y0 = 0): the three nonzero kernel elements + s; L = 4: the four
+    // solutions y, X = 1/y + s (a != 0) or y.  Selects, every X[i] written: a store per case
+    // would be merged into one indexed by L, in scratch memory.
+    const bool l3 = L == 3, inv = L == 4 && a;
+    const uint32_t y[4] = {l3 ? k1 : y0, l3 ? k2 : y0 ^ k1, l3 ? k1 ^ k2 : y0 ^ k2, y0 ^ k1 ^ k2};
 #pragma unroll
-    for (int i = 0; i < 4; ++i) X[i] = a ? f.inv(y[i]) ^ s : y[i];
-    return 4;
+    for (int i = 0; i < 4; ++i) X[i] = inv ? f.inv(y[i] ? y[i] : 1u) ^ s : (l3 ? y[i] ^ s : y[i]);
+    return L;
 }
 
 // Chien search over the codeword's bit positions p < nbits: X = alpha^p is a root of
