@@ -644,18 +644,25 @@ __global__ void __launch_bounds__(kThreads) k_bch_decode(DevBch b, BchArgs a) {
 // flipped in the tile's LDS image, and after a workgroup barrier each row writes back the 16-byte
 // pieces of the global grid that hold its flips -- a piece reaching outside the tile's bytes only
 // over the tile's own, byte by byte.  One pass over the rows: read once, corrected pieces written.
+// One tile image per workgroup and three workgroups per CU: the per-row locate is a chain of
+// dependent table reads, and a third wave per SIMD hides more of it than a second image hides of
+// the DMA (8 M: 0.644 vs 0.780 ms with two images and two workgroups per CU, r06r)
+constexpr int kDecSlots = 1;
+constexpr int kDecLds = kDecSlots * ezrs::bps::kImgSlot + ezrs::bps::kTW * ezrs::bps::kXch;
+constexpr int kDecPerCu = 3;                   // workgroups per CU (LDS)
+
 template <class C>
-__global__ void __launch_bounds__(64 * ezrs::bps::kTW) k_bch_ps_decode(DevBch b, BchArgs a, BpsArgs p) {
+__global__ void __launch_bounds__(64 * ezrs::bps::kTW, kDecPerCu) k_bch_ps_decode(DevBch b, BchArgs a, BpsArgs p) {
     namespace bp = ezrs::bps;
     constexpr int TW = bp::tile_waves<C>(), T = C::T, NR = 4 / TW;
     constexpr uint32_t n = (1u << C::M) - 1;
     static_assert(T <= 4, "odd syndromes S1 .. S7 from the nibble tables");
     constexpr uint32_t kTabs = ((3 * n + 1) * 2 + 15) / 16 * 16, kNib = 2 * C::EB * 16;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[bp::kLds + kTabs + 8 * kNib];
-    uint16_t *ex = reinterpret_cast<uint16_t *>(lds + bp::kLds), *lg = ex + 2 * n;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kDecLds + kTabs + 8 * kNib];
+    uint16_t *ex = reinterpret_cast<uint16_t *>(lds + kDecLds), *lg = ex + 2 * n;
     // syndrome tables by nibble of the remainder (from the top): the byte tables are linear in the
     // byte, so nibble q's entry for v is the byte table's for v << 4 (q even) or v
-    uint64_t *nib = reinterpret_cast<uint64_t *>(lds + bp::kLds + kTabs);
+    uint64_t *nib = reinterpret_cast<uint64_t *>(lds + kDecLds + kTabs);
     for (uint32_t i = threadIdx.x; i < 2 * n; i += blockDim.x) ex[i] = b.ex[i];
     for (uint32_t i = threadIdx.x; i <= n; i += blockDim.x) lg[i] = b.lg[i];
     for (uint32_t i = threadIdx.x; i < kNib; i += blockDim.x) {
@@ -667,7 +674,7 @@ __global__ void __launch_bounds__(64 * ezrs::bps::kTW) k_bch_ps_decode(DevBch b,
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = bp::lane_id();
     const uint32_t nbits = 8u * a.len + (uint32_t)b.ecc_bits, tb = bp::kRows * p.stride;
     // rows 4l + k, k = w (TW = 4) or 2w, 2w + 1
-    bp::tile_loop<C, true, -1>(p, lds, [&](uint32_t tile, uint8_t *image, const uint32_t (&out)[C::EB]) {
+    bp::tile_loop<C, true, -1, kDecSlots>(p, lds, [&](uint32_t tile, uint8_t *image, const uint32_t (&out)[C::EB]) {
         uint32_t loc[NR][T];
         int cnt[NR];
 #pragma unroll
@@ -1255,7 +1262,7 @@ hipError_t launch_encode(const DevBch &b, BchArgs a, hipStream_t s) {
 }
 
 hipError_t launch_bps_decode(const DevBch &b, const BchArgs &a, const BpsArgs &p, hipStream_t s) {
-    const unsigned cap = 2u * (unsigned)(b.ncu > 0 ? b.ncu : 256);         // 2 workgroups per CU (LDS)
+    const unsigned cap = (unsigned)kDecPerCu * (unsigned)(b.ncu > 0 ? b.ncu : 256);
     const unsigned grid = p.ntiles < cap ? p.ntiles : cap;
     if (!grid) return hipSuccess;
     int k = 0;

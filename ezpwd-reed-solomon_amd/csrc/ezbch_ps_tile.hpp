@@ -185,9 +185,13 @@ template <int EB> struct EccStore {
 // byte e of the ECC (encode) or of the remainder XOR the received ECC (decode) of row
 // tile * 256 + 4l + k, and image[j] (LDS) is byte tile * 256 * stride + j of the batch.  NV: the
 // vector-memory instructions fin issues per tile, left in flight by the next tile's wait, or -1
-// when their number varies (the wait then takes them all).
-template <class C, bool DEC, int NV, class Fin>
+// when their number varies (the wait then takes them all).  NSLOT: 2 -- the next tile's rows land
+// in the other image while this one is computed; 1 -- one image (X = its offset in lds), the next
+// tile's DMA issued once fin is done with it (three workgroups per CU cover each other's waits).
+template <class C, bool DEC, int NV, int NSLOT = 2, class Fin>
 __device__ __forceinline__ void tile_loop(const BpsArgs &a, uint8_t *lds, Fin &&fin) {
+    static_assert(NSLOT == 1 || NSLOT == 2, "one or two images");
+    constexpr uint32_t kX = NSLOT * kImgSlot;             // exchange words after the images
     constexpr int TW = tile_waves<C>();
     static_assert(C::NB % (2 * TW) == 0 && (TW == 2 || TW == 4) && C::F <= 128 && C::EB <= 8,
                   "frame: whole 16-position pieces per wave");
@@ -209,7 +213,7 @@ __device__ __forceinline__ void tile_loop(const BpsArgs &a, uint8_t *lds, Fin &&
     if (tile < a.ntiles) issue(tile, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     for (uint32_t it = 0; tile < a.ntiles; ++it, tile += gridDim.x) {
-        const uint32_t slot = it & 1, img = lds0 + slot * kImgSlot + kGuard;
+        const uint32_t slot = NSLOT == 2 ? (it & 1) : 0u, img = lds0 + slot * kImgSlot + kGuard;
         // this wave's share of the tile's DMA (issued an iteration ago) has landed; the last tile's
         // fin may leave its stores in flight
         if constexpr (NV >= 0) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NV) : "memory");
@@ -229,7 +233,7 @@ __device__ __forceinline__ void tile_loop(const BpsArgs &a, uint8_t *lds, Fin &&
         // exchange words
         asm volatile("s_barrier" ::: "memory");
         const uint32_t nt = tile + gridDim.x;
-        if (nt < a.ntiles) issue(nt, slot ^ 1);
+        if (NSLOT == 2 && nt < a.ntiles) issue(nt, slot ^ 1);
         int fb = a.fb;
         asm volatile("" : "+s"(fb));
         uint32_t U[C::E];
@@ -253,7 +257,7 @@ __device__ __forceinline__ void tile_loop(const BpsArgs &a, uint8_t *lds, Fin &&
             out[e] = v;
         }
         // the other waves' partial bytes
-        uint32_t *xw = (uint32_t *)(lds + 2 * kImgSlot);
+        uint32_t *xw = (uint32_t *)(lds + kX);
 #pragma unroll
         for (int e = 0; e < C::EB; ++e) xw[w * (kXch / 4) + e * 64 + l] = out[e];
         __syncthreads();
@@ -264,6 +268,12 @@ __device__ __forceinline__ void tile_loop(const BpsArgs &a, uint8_t *lds, Fin &&
             for (int e = 0; e < C::EB; ++e) out[e] ^= xw[p * (kXch / 4) + e * 64 + l];
         }
         fin(tile, lds + slot * kImgSlot + kGuard, out);
+        if constexpr (NSLOT == 1) {
+            if (nt < a.ntiles) {
+                asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // fin is done with the image
+                issue(nt, 0);
+            }
+        }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");        // no DMA may land after the exit
 }
