@@ -260,15 +260,19 @@ __global__ void __launch_bounds__(kThreads) k_bch_encode(DevBch b, BchArgs a) {
 // y -> A4 y^4 + A2 y^2 + A1 y is GF(2)-linear.  With the images of the polynomial-basis vectors
 // 1 << i (= alpha^i) in echelon form: returns the kernel dimension, or -1 if A(y) = delta has no
 // solution; y0 = a particular solution, k1, k2 = the first two kernel basis vectors.
+// MM: m known at compile time (the plane-sliced decode's codec), or 0
+template <int MM = 0>
 __device__ int solve_affine(const GF &f, int m, uint32_t A4, uint32_t A2, uint32_t A1,
                             uint32_t delta, uint32_t &y0, uint32_t &k1, uint32_t &k2) {
+    constexpr int kM = MM ? MM : kMaxM;
+    if constexpr (MM != 0) m = MM;
     const int l4 = A4 ? (int)f.lg[A4] : -1, l2 = A2 ? (int)f.lg[A2] : -1, l1 = A1 ? (int)f.lg[A1] : -1;
-    uint32_t v[kMaxM], c[kMaxM];
-    int pb[kMaxM];
+    uint32_t v[kM], c[kM];
+    int pb[kM];
     int dim = 0;
     uint32_t q1 = 0, q2 = 0;                // k1, k2: selects, not a store indexed by dim (scratch)
 #pragma unroll
-    for (int i = 0; i < kMaxM; ++i) {
+    for (int i = 0; i < kM; ++i) {
         v[i] = 0;
         c[i] = 0;
         pb[i] = -1;
@@ -294,7 +298,7 @@ __device__ int solve_affine(const GF &f, int m, uint32_t A4, uint32_t A2, uint32
     }
     uint32_t y = 0, rem = delta;
 #pragma unroll
-    for (int k = 0; k < kMaxM; ++k)
+    for (int k = 0; k < kM; ++k)
         if (pb[k] >= 0 && ((rem >> pb[k]) & 1u)) {
             rem ^= v[k];
             y ^= c[k];
@@ -307,6 +311,7 @@ __device__ int solve_affine(const GF &f, int m, uint32_t A4, uint32_t A2, uint32
 
 // Roots X of sigma(X) = X^L + a X^(L-1) + b X^(L-2) + c X^(L-3) + d for L = 2..4 (sigma(0) != 0);
 // returns L if there are L distinct roots, else 0.
+template <int MM = 0>
 __device__ int small_roots(const GF &f, int m, int L, uint32_t a, uint32_t b, uint32_t c, uint32_t d,
                            uint32_t (&X)[4]) {
     uint32_t A4, A2, A1, delta, s = 0;
@@ -326,7 +331,7 @@ __device__ int small_roots(const GF &f, int m, int L, uint32_t a, uint32_t b, ui
         A4 = 1; A2 = f.mul(f.mul(a, s) ^ b, ie); A1 = f.mul(a, ie); delta = ie; want = 2;
     }
     uint32_t y0, k1, k2;
-    if (solve_affine(f, m, A4, A2, A1, delta, y0, k1, k2) != want) return 0;
+    if (solve_affine<MM>(f, m, A4, A2, A1, delta, y0, k1, k2) != want) return 0;
     // L = 2: y0, y0 + k1; L = 3 (y0 = 0): the three nonzero kernel elements + s; L = 4: the four
     // solutions y, X = 1/y + s (a != 0) or y.  Selects, every X[i] written: a store per case
     // would be merged into one indexed by L, in scratch memory.
@@ -373,7 +378,7 @@ __device__ __forceinline__ uint32_t coef(const uint32_t (&C)[W]) {
 
 // decode_bch on the masked ECC difference r (left-justified): the count and the ascending error
 // locations, or -EBADMSG.
-template <int T, int NW>
+template <int T, int NW, int MM = 0>
 __device__ int locate(const DevBch &b, const GF &f, Rem<NW> r, uint32_t nbits,
                       uint32_t (&loc)[T], const uint32_t *sin = nullptr) {
     uint64_t any = 0;
@@ -523,7 +528,7 @@ __device__ int locate(const DevBch &b, const GF &f, Rem<NW> r, uint32_t nbits,
         nr = 1;
     } else if (L <= 4) {
         uint32_t X[4];
-        nr = small_roots(f, b.m, L, C[1], C[2], coef<3>(C), coef<4>(C), X);
+        nr = small_roots<MM>(f, b.m, L, C[1], C[2], coef<3>(C), coef<4>(C), X);
 #pragma unroll
         for (int i = 0; i < T && i < 4; ++i)
             if (i < nr) P[i] = f.lg[X[i]];
@@ -697,7 +702,7 @@ __global__ void __launch_bounds__(64 * ezrs::bps::kTW, kDecPerCu) k_bch_ps_decod
                 for (int jj = 1; jj < 2 * T; jj += 2) S[jj - 1] = (uint32_t)(acc >> (8 * (jj - 1))) & 0xFFFFu;
 #pragma unroll
                 for (int jj = 1; jj <= T; ++jj) S[2 * jj - 1] = f.sq(S[jj - 1]);
-                c = locate<T, 1>(b, f, rm, nbits, loc[j], S);
+                c = locate<T, 1, C::M>(b, f, rm, nbits, loc[j], S);
             }
             a.result[row] = c;
             if (c <= 0) continue;
