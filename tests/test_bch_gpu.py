@@ -322,3 +322,39 @@ def test_c5_packed_rows_at_odd_offset(torch):
         g = guard.cpu().numpy()
         np.testing.assert_array_equal(f[:off], g[:off])
         np.testing.assert_array_equal(f[off + ncw * (L + eb):], g[off + ncw * (L + eb):])
+
+
+@pytest.mark.parametrize("ncw", [1, 2, 5, 255, 256, 257, 767])
+def test_c5_plane_sliced_small_batches(torch, ncw):
+    """The plane-sliced encode and fused decode (ezbch_ps_tile.hpp) on batches of one partial tile,
+    exactly one, and a few: the first tile's guard bytes, the span-end re-read of the last row, rows
+    past the batch dropped by the buffer range checks.  Encode into packed rows (ECC inline) and
+    into a separate ECC array, then decode 0..4 (and 5, uncorrectable) bit errors per row against
+    the oracle, with error locations."""
+    import ezrs
+    oc, c = O.BCH(10, 4), ezrs.BCH.nkt(1023, 983, 4)
+    L, eb = 122, 5
+    rng = np.random.default_rng(0xC5 + ncw)
+    rows = rng.integers(0, 256, (ncw, L + eb), dtype=np.uint8)
+    ref = rows.copy()
+    oc.encode_batch(ref, L, nthreads=8)
+    dev = torch.from_numpy(rows).cuda()
+    c.encode(dev, L)                                      # ECC inline
+    np.testing.assert_array_equal(dev.cpu().numpy(), ref)
+    data = torch.from_numpy(np.ascontiguousarray(rows[:, :L])).cuda()
+    ecc = torch.zeros((ncw, eb), dtype=torch.uint8, device="cuda")
+    c.encode(data, L, ecc=ecc)                            # separate ECC array
+    np.testing.assert_array_equal(ecc.cpu().numpy(), ref[:, L:])
+    bad = ref.copy()
+    _flip(bad, 8 * L + oc.ecc_bits, np.arange(ncw) % 6, rng)
+    exp = bad.copy()
+    eloc = np.zeros((ncw, 4), np.uint32)
+    eres = oc.decode_batch(exp, L, errloc=eloc, nthreads=8)
+    d = torch.from_numpy(bad).cuda()
+    loc = torch.zeros((ncw, 4), dtype=torch.int32, device="cuda")
+    res = c.decode(d, L, errloc=loc).cpu().numpy()
+    np.testing.assert_array_equal(res, eres)
+    np.testing.assert_array_equal(d.cpu().numpy(), exp)
+    got = loc.cpu().numpy().view(np.uint32)
+    for k in np.nonzero(eres > 0)[0]:
+        np.testing.assert_array_equal(got[k, :eres[k]], eloc[k, :eres[k]])
