@@ -1,0 +1,13 @@
+set -u
+cd $GRAFT_REPO_ROOT
+export EZRS_LIB_VARIANT=$GRAFT_REPO_ROOT/tools/variants/libezrs_pq251.so
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 240 --timeout-method thread -k "251" > gpurun_out/r06y_pytest.log 2>&1
+rc=$?; echo "variant parity rc=$rc: $(tail -n 1 gpurun_out/r06y_pytest.log)"; [ $rc -eq 0 ] || exit $rc
+for rep in 1 2; do
+  for v in default pq251; do
+    if [ $v = default ]; then unset EZRS_LIB_VARIANT; else export EZRS_LIB_VARIANT=$GRAFT_REPO_ROOT/tools/variants/libezrs_$v.so; fi
+    timeout -k 10 200 python bench.py --workload c1 --steps 200 --warmup 20 --no-cpu-baseline > gpurun_out/r06y_c1_$v.json 2>/dev/null || exit 1
+    python3 -c "
+import json; d=json.loads(open('gpurun_out/r06y_c1_$v.json').read().splitlines()[-1]); print('$rep $v', d['value'], d['roofline']['avg_ms'])"
+  done
+done
