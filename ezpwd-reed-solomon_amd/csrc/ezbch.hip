@@ -438,10 +438,6 @@ __device__ int locate(const DevBch &b, const GF &f, Rem<NW> r, uint32_t nbits,
         B[j] = j == 1;
     }
     int L = 0;
-#ifndef EZRS_BCH_BM_LOG
-#define EZRS_BCH_BM_LOG 1
-#endif
-#if EZRS_BCH_BM_LOG
     // Log domain: the syndromes' logs once (an even one is twice the log of its half), the
     // discrepancy's quotient by its log, and only the coefficients that can be nonzero: before odd
     // step rr, deg C <= rr - 1 and deg B <= rr (B = x at rr = 1; C + q B, x^2 C, x^2 B keep it),
@@ -485,34 +481,6 @@ __device__ int locate(const DevBch &b, const GF &f, Rem<NW> r, uint32_t nbits,
             for (int j = W - 1; j >= 0; --j) B[j] = j >= 2 ? B[j - 2] : 0u;
         }
     }
-#else
-    uint32_t bd = 1;
-#pragma unroll
-    for (int rr = 1; rr < 2 * T; rr += 2) {
-        uint32_t d = S[rr];
-#pragma unroll
-        for (int i = 1; i < rr; ++i) d ^= f.mul(C[i], S[rr - i]);
-        if (d) {
-            const bool grow = 2 * L <= rr - 1;
-            const uint32_t q = f.div(d, bd);
-            uint32_t old[W];
-#pragma unroll
-            for (int j = 0; j < W; ++j) {
-                old[j] = C[j];
-                C[j] ^= f.mul(q, B[j]);
-            }
-            if (grow) {
-                L = rr - L;
-                bd = d;
-            }
-#pragma unroll
-            for (int j = W - 1; j >= 0; --j) B[j] = j >= 2 ? (grow ? old[j - 2] : B[j - 2]) : 0u;
-        } else {
-#pragma unroll
-            for (int j = W - 1; j >= 0; --j) B[j] = j >= 2 ? B[j - 2] : 0u;
-        }
-    }
-#endif
     if (L > T) return -kEBADMSG;
     if (L == 0) return 0;
     uint32_t lead = 0;

@@ -378,25 +378,7 @@ __global__ void __launch_bounds__(256)
         if (k >= ncw) break;
         uint8_t *dst = parity + k * pstride;
         const uint8_t *src8 = stage + (r >> 5) * kRegion + (r & 31) * C::NR;
-#ifndef EZRS_PARITY_STORE
-#define EZRS_PARITY_STORE 0
-#endif
-        if constexpr (EZRS_PARITY_STORE == 2) {          // timing-only: no stores
-            if (src8[0] == 0xA5 && k == 0x7FFFFFFFFFFFull) dst[0] = 0;
-        } else if constexpr (EZRS_PARITY_STORE == 1 && C::NR % 4 == 0) {
-            // byte stores up to the first aligned dword, aligned dword stores, byte stores after
-            const unsigned h = (4u - (unsigned)((uintptr_t)dst & 3u)) & 3u;
-            const uint32_t *s32 = reinterpret_cast<const uint32_t *>(src8);
-            for (unsigned o = 0; o < h; ++o) dst[o] = src8[o];
-            uint32_t *d32 = reinterpret_cast<uint32_t *>(dst + h);
-            constexpr unsigned NW = C::NR / 4;
-#pragma unroll
-            for (unsigned i = 0; i + 1 < NW; ++i)
-                d32[i] = __builtin_amdgcn_alignbyte(s32[i + 1], s32[i], h);
-            if (h == 0) d32[NW - 1] = s32[NW - 1];
-            else
-                for (unsigned o = h + 4 * (NW - 1); o < C::NR; ++o) dst[o] = src8[o];
-        } else if constexpr (C::NR % 16 == 0) {
+        if constexpr (C::NR % 16 == 0) {
 #pragma unroll
             for (int o = 0; o < C::NR; o += 16) {
                 uint4 v = *reinterpret_cast<const uint4 *>(src8 + o);

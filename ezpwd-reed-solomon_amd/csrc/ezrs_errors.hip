@@ -42,15 +42,6 @@ constexpr int32_t kSentinel = INT32_MIN;
 #ifndef EZRS_ERR_STOP
 #define EZRS_ERR_STOP 0                 // timing ablations (variant builds only): see decode_lane
 #endif
-#ifndef EZRS_ERR_OMSL
-#define EZRS_ERR_OMSL 1                 // Omega: the syndromes' logs read once into registers
-#endif
-#ifndef EZRS_ERR_BMMASK
-#define EZRS_ERR_BMMASK 1
-#endif
-#ifndef EZRS_ERR_NOCACHE
-#define EZRS_ERR_NOCACHE 0
-#endif
 
 constexpr int kSpan = 256;              // result slots screened per wavefront
 constexpr int kWaves = 16;              // wavefronts per workgroup (one workgroup per CU)
@@ -216,7 +207,7 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
 #pragma unroll
         for (int i0 = 0; i0 <= 32; i0 += 4) {
             if ((unsigned)i0 <= dmax) {
-                if (EZRS_ERR_NOCACHE || (unsigned)i0 + 3u > lhi) {
+                if ((unsigned)i0 + 3u > lhi) {
 #pragma unroll
                     for (int i = i0; i < i0 + 4 && i <= 32; ++i) l[i] = i == 0 ? 0u : gi(L, lam[i]);
                 }
@@ -228,7 +219,6 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
         const unsigned dl = gi(L, discr);
         const bool upd = dl < 510u && 2 * el <= r + no_eras - 1;
         const unsigned ndl = 255u - dl;
-#if EZRS_ERR_BMMASK
         // lambda += Delta x B only in the lanes whose discrepancy is nonzero: the others issue no
         // table reads (a zero discrepancy is the rule past step 2 nu + ne of a decodable word)
         if (dl < 510u) {
@@ -254,22 +244,6 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
                 }
             }
         }
-#else
-#pragma unroll
-        for (int i0 = 32; i0 >= 0; i0 -= 4) {
-            if ((unsigned)i0 <= umax) {
-#pragma unroll
-                for (int i = i0 + 3; i >= i0; --i) {
-                    if (i > 32) continue;
-                    const unsigned bp = i > 0 ? b[i - 1] : kZ;
-                    if (i > 0) lam[i] ^= gp(L, (dl + bp));
-                    const unsigned d = l[i] + ndl;
-                    const unsigned nb = min(min(d, d - 255u), kZ);
-                    b[i] = upd ? nb : bp;
-                }
-            }
-        }
-#endif
         if (dl < 510u) lhi = 0;               // this lane's lambda changed
         el = upd ? r + no_eras - el : el;
     }
@@ -347,7 +321,7 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
         for (int i0 = 0; i0 < 32; i0 += 4) {
             if ((unsigned)i0 <= deg_omega) {
 #pragma unroll
-                for (int i = i0; i < i0 + 4; ++i) sl[i] = EZRS_ERR_OMSL ? S(31 - i) : 0u;
+                for (int i = i0; i < i0 + 4; ++i) sl[i] = S(31 - i);
             }
         }
 #pragma unroll
@@ -358,7 +332,7 @@ __device__ __attribute__((always_inline)) int decode_lane(const DevCodec &c, con
                     unsigned t = 0;
                     if ((unsigned)i <= deg_omega) {      // (lanes past their degree read nothing)
 #pragma unroll
-                        for (int j = 0; j <= i; ++j) t ^= gp(L, ((EZRS_ERR_OMSL ? sl[i - j] : S(31 - (i - j))) + l[j]));
+                        for (int j = 0; j <= i; ++j) t ^= gp(L, (sl[i - j] + l[j]));
                     }
                     om[i] = gi(L, t);
                 }

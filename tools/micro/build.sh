@@ -8,6 +8,4 @@ $H -x hip -DEZRS_BS_ABLATE_DMA $D/bs_ablate.cpp -o $D/bs_ablate_nodma &
 $H -x hip -DEZRS_BS_ABLATE_COMPUTE $D/bs_ablate.cpp -o $D/bs_ablate_nocomp &
 $H -x hip -DEZRS_BS_ABLATE_TRANSPOSE $D/bs_ablate.cpp -o $D/bs_ablate_notr &
 $H -x hip -DEZRS_BS_ABLATE_DMA -DEZRS_BS_ABLATE_TRANSPOSE $D/bs_ablate.cpp -o $D/bs_ablate_computeonly &
-$H -x hip -DEZRS_PARITY_STORE=1 $D/bs_ablate.cpp -o $D/bs_ablate_pst1 &
-$H -x hip -DEZRS_PARITY_STORE=2 $D/bs_ablate.cpp -o $D/bs_ablate_nostore &
 wait
