@@ -577,7 +577,7 @@ def gen_pt(c: PsCodec):
 # ---- 4-wave tile kernel (k_pq): each wave evaluates ALL leaders over its own run of positions ------
 PQ_WAVES = 4
 PQ_XCAP = 8               # items a wave sends per exchange sub-round (4 x 8 x 2 KiB = the 64 KiB image)
-PQ_CODECS = {"RS_255_223", "RS_255_251", "RS_255_239"}
+PQ_CODECS = {"RS_255_223", "RS_255_251", "RS_255_239", "RS_255_247", "RS_255_243", "RS_255_238", "RS_255_228", "CCSDS_CONV_255_239"}
 
 
 def gen_pq(c: PsCodec):
